@@ -1,0 +1,154 @@
+/*
+ * xerus_amd.h — C-ABI of the MI355X-native xerus hot path (dense contraction + TT rounding).
+ *
+ * The reference (xerus v3.0.1, /root/reference) has no plugin registry; its narrowest internal
+ * boundary is the free-function namespace xerus::blasWrapper over raw row-major double*
+ * (include/xerus/blasLapackWrapper.h:37-146) plus the Tensor-level reshuffle/contract
+ * (include/xerus/tensor.h:56-66). Every entry point below replaces one of those and cites it.
+ *
+ * Conventions (identical to the reference unless stated):
+ *   - element type double (include/xerus/basic.h:44), all matrices ROW-MAJOR, dims are size_t;
+ *   - every data pointer is a DEVICE pointer (allocated with xrs_malloc or any hipMalloc'd memory
+ *     of the handle's device); host<->device traffic happens only in xrs_upload/xrs_download and
+ *     in the few functions that return a scalar (documented per function);
+ *   - work is enqueued on the handle's stream; functions that must return a host value
+ *     (rank, norm) synchronise that stream;
+ *   - return value: 0 = ok, < 0 = argument error (reference: XERUS_REQUIRE -> generic_error,
+ *     misc/check.h:60-65), > 0 = numerical failure (reference: LAPACK info != 0,
+ *     blasLapackWrapper.cpp:263,290,409). xrs_last_error() returns the message of the last
+ *     failure on the calling host thread.
+ *   - the library never frees caller buffers (SURVEY §8(b) "Ownership"). Functions that must
+ *     allocate because the rank is data dependent (QC/CQ, TT round) write into caller-provided
+ *     buffers sized for the maximal rank min(m,n) and return the rank.
+ *   - one handle per host thread (a stream + a caching device allocator); no global mutable state
+ *     besides the thread-local error string.
+ */
+#ifndef XERUS_AMD_H
+#define XERUS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct xrs_handle_s* xrs_handle_t;
+
+#define XRS_OK 0
+#define XRS_EINVAL (-1)      /* illegal argument (reference: REQUIRE failure)           */
+#define XRS_ENOMEM (-2)      /* device allocation failed                                */
+#define XRS_EHIP (-3)        /* HIP runtime error                                       */
+#define XRS_ENUMERIC 1       /* numerical failure (reference: LAPACK info != 0)          */
+
+/* ---------------------------------------------------------------- runtime */
+/** Create a handle on device `device` with its own non-blocking stream. */
+int xrs_create(xrs_handle_t* handle, int device);
+int xrs_destroy(xrs_handle_t handle);
+/** Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream). NULL = own stream. */
+int xrs_set_stream(xrs_handle_t handle, void* hip_stream);
+void* xrs_get_stream(xrs_handle_t handle);
+int xrs_synchronize(xrs_handle_t handle);
+const char* xrs_last_error(void);
+const char* xrs_version(void);
+
+/** Stream-ordered caching allocator of the handle (blocks are reused, never hipFree'd in flight). */
+int xrs_malloc(xrs_handle_t handle, void** ptr, size_t bytes);
+int xrs_free(xrs_handle_t handle, void* ptr);
+/** Bytes currently held by the handle's pool (in use + cached). */
+size_t xrs_pool_bytes(xrs_handle_t handle);
+int xrs_upload(xrs_handle_t handle, double* dst_dev, const double* src_host, size_t n);
+int xrs_download(xrs_handle_t handle, double* dst_host, const double* src_dev, size_t n);
+int xrs_memset_zero(xrs_handle_t handle, double* dst_dev, size_t n);
+int xrs_copy(xrs_handle_t handle, double* dst_dev, const double* src_dev, size_t n);
+
+/* ---------------------------------------------------------------- level 1 (blasLapackWrapper.h:42-48) */
+/** *result = ||x||_2   (replaces blasWrapper::two_norm, blasLapackWrapper.cpp:88-98). Synchronises. */
+int xrs_nrm2(xrs_handle_t handle, double* result, const double* x, size_t n);
+/** *result = x^T y     (replaces blasWrapper::dot_product, blasLapackWrapper.cpp:101-110). Synchronises. */
+int xrs_dot(xrs_handle_t handle, double* result, const double* x, const double* y, size_t n);
+/** *result = ||x||_1   (replaces blasWrapper::one_norm, blasLapackWrapper.cpp:76-86). Synchronises. */
+int xrs_asum(xrs_handle_t handle, double* result, const double* x, size_t n);
+/** x *= alpha          (replaces misc::scale / Tensor::apply_factor, misc/basicArraySupport.h:60-70). */
+int xrs_scal(xrs_handle_t handle, double* x, double alpha, size_t n);
+/** y += alpha*x        (replaces misc::add_scaled, misc/basicArraySupport.h:90-110). */
+int xrs_axpy(xrs_handle_t handle, double* y, double alpha, const double* x, size_t n);
+/** X[i,:] *= s[i], X is m x n (replaces the diag(S)*dense product of round_edge,
+ *  sparseTimesFullContraction.cpp:66-96 dispatched from tensorNetwork.cpp:769). */
+int xrs_scale_rows(xrs_handle_t handle, double* X, const double* s, size_t m, size_t n);
+
+/* ---------------------------------------------------------------- level 3 (blasLapackWrapper.h:61-85) */
+/** C = alpha * op(A) * op(B), beta = 0, row-major, ldc = N.
+ *  Replaces blasWrapper::matrix_matrix_product (blasLapackWrapper.cpp:149-195) with the same
+ *  argument order: M = _leftDim, N = _rightDim, K = _middleDim, lda = transA ? M : K in the inline
+ *  overload (blasLapackWrapper.h:74-85). The reference delegates M==1 / N==1 to GEMV and K==1 to
+ *  GER (:161-166); here every shape goes through the MFMA kernel family (results equal within
+ *  rounding). C must not alias A or B. */
+int xrs_gemm(xrs_handle_t handle, double* C, size_t M, size_t N, double alpha,
+             const double* A, size_t lda, int transA, size_t K,
+             const double* B, size_t ldb, int transB);
+
+/* ---------------------------------------------------------------- permutation (tensor.h:65) */
+/** out = reshuffle(in, shuffle): out[...] with mode i of `in` moved to position shuffle[i]
+ *  (indexedTensor_tensor_evaluate.cpp:55-143; shuffle[i] = NEW position of OLD mode i, :80-82).
+ *  Bit-exact. `dims` are the dims of `in`. out must not alias in. */
+int xrs_permute(xrs_handle_t handle, double* out, const double* in, size_t ndim,
+                const size_t* dims, const size_t* shuffle);
+
+/* ---------------------------------------------------------------- factorisations (blasLapackWrapper.h:90-135) */
+/** Rank-revealing A = Q*C for an m x n matrix (replaces blasWrapper::qc, blasLapackWrapper.cpp:235-305).
+ *  Q: m x rank, orthonormal columns; C: rank x n. Rank rule of the reference (:268-272):
+ *  the first k with |R_kk| < 16*DBL_EPSILON*R_00 of the column-pivoted QR (dgeqp3 sign convention).
+ *  Q must hold m*min(m,n) doubles, C min(m,n)*n; on return they are packed with leading dims
+ *  rank and n. *rank is written on the host. Synchronises. */
+int xrs_qc(xrs_handle_t handle, double* Q, double* C, size_t* rank, const double* A, size_t m, size_t n);
+/** A = C*Q, C: m x rank, Q: rank x n orthonormal rows (replaces blasWrapper::cq, :308-371;
+ *  pivoting over the rows of A as the reference's col-major dgeqp3 on A^T). Synchronises. */
+int xrs_cq(xrs_handle_t handle, double* C, double* Q, size_t* rank, const double* A, size_t m, size_t n);
+/** Unpivoted A = Q*R, Q: m x min(m,n), R: min(m,n) x n (replaces blasWrapper::qr, :374-431). */
+int xrs_qr(xrs_handle_t handle, double* Q, double* R, const double* A, size_t m, size_t n);
+/** Unpivoted A = R*Q, R: m x min(m,n), Q: min(m,n) x n (replaces blasWrapper::rq, :445-498). */
+int xrs_rq(xrs_handle_t handle, double* R, double* Q, const double* A, size_t m, size_t n);
+/** Thin SVD A = U*diag(S)*Vt, U: m x k, S: k, Vt: k x n, k = min(m,n), S descending
+ *  (replaces blasWrapper::svd / dgesdd 'S', blasLapackWrapper.cpp:201-232). */
+int xrs_svd(xrs_handle_t handle, double* U, double* S, double* Vt, const double* A, size_t m, size_t n);
+
+/* ---------------------------------------------------------------- TT hot path (ttNetwork.cpp) */
+/* A TT of order d is passed as d device core pointers; core k has dims (r[k], n[k], r[k+1]),
+ * r[0] = r[d] = 1 (ttNetwork.cpp:57-108, 457-460). Functions that change ranks allocate NEW cores
+ * from the handle's pool, write their pointers into `cores` and free the old ones with xrs_free
+ * (the caller owns the result and releases it with xrs_free). */
+
+/** Left-to-right / right-to-left orthogonalisation moving the core to `position`
+ *  (TTNetwork::move_core, ttNetwork.cpp:582-628, transfer_core tensorNetwork.cpp:821-909).
+ *  `canonicalized`/`core_position` describe the input state as in the reference (:588-607). */
+int xrs_tt_move_core(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
+                     int canonicalized, size_t core_position, size_t position, int keep_rank);
+/** TTNetwork::round(maxRanks, eps) (ttNetwork.cpp:644-665): canonicalise right, then truncate
+ *  every edge right-to-left keeping at most max_ranks[k] singular values and cutting
+ *  sigma_j <= eps*sigma_0 (tensor.cpp:1463-1474). On return the core is at position 0. */
+int xrs_tt_round(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
+                 int canonicalized, size_t core_position, const size_t* max_ranks, double eps);
+/** <x,y> of two TTs with equal mode sizes (value_t(x(i&0)*y(i&0)), ttNetwork.cpp:782-789 path,
+ *  SURVEY §3.4) as a left-to-right zipper without permutations. *result on host. Synchronises. */
+int xrs_tt_dot(xrs_handle_t handle, double* result, size_t d, const size_t* n,
+               const size_t* rx, const double* const* xcores,
+               const size_t* ry, const double* const* ycores);
+
+/* ---------------------------------------------------------------- profiling */
+/** Kernel-duration instrumentation: while enabled, every launch of a kernel whose family id is in
+ *  `family_mask` is bracketed by HIP events on the handle's stream. */
+#define XRS_KFAM_GEMM 1u
+#define XRS_KFAM_PERMUTE 2u
+#define XRS_KFAM_QR 4u
+#define XRS_KFAM_SVD 8u
+#define XRS_KFAM_ELEMWISE 16u
+int xrs_prof_begin(xrs_handle_t handle, uint32_t family_mask);
+/** Stops instrumentation, synchronises and returns (launches, total kernel milliseconds,
+ *  algorithmic flops, algorithmic bytes) of the instrumented launches. */
+int xrs_prof_end(xrs_handle_t handle, size_t* launches, double* total_ms, double* flops, double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XERUS_AMD_H */

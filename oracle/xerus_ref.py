@@ -1,0 +1,394 @@
+"""CPU oracle: a restatement of the reference's algorithms on the hot path.
+
+TEST INFRASTRUCTURE ONLY. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker / the timed CPU baseline — never as the product path.
+
+Every function cites the reference file:line it follows (reference: xerus v3.0.1 at
+/root/reference, which is NOT available at run time on the GPU box). The linear algebra calls the
+same LAPACK routines the reference calls through LAPACKE (dgeqp3, dorgqr, dgeqrf, dgerqf, dorgrq,
+dgesdd — via scipy.linalg.lapack, scipy-openblas 0.3.29) and BLAS dgemm (numpy). The byte-exact
+pieces (reshuffle, Tensor::random's input stream) are restated in C (oracle/csrc/oracle.c).
+
+Pinning: the reference itself is unbuildable in this image (it needs cblas.h/lapacke.h, SuiteSparse
+CHOLMOD and Boost headers that are absent), so this oracle is pinned by the
+reference's own known-answer tests re-expressed as data in tests/golden/ (products, assignments,
+factorisation properties, TT rounding properties) and by the libstdc++ RNG stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+from scipy.linalg import lapack
+
+DBL_EPSILON = float(np.finfo(np.float64).eps)
+EPSILON = 8 * DBL_EPSILON  # include/xerus/basic.h:51
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            import subprocess
+
+            subprocess.run(["make", "-s", "-C", _HERE], check=True)
+        lib = C.CDLL(path)
+        lib.orc_reshuffle.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+        lib.orc_rng_seed.argtypes = [C.c_void_p, C.c_uint64]
+        lib.orc_rng_seed_engine.argtypes = [C.c_void_p, C.c_uint64]
+        lib.orc_rng_next.argtypes = [C.c_void_p]
+        lib.orc_rng_next.restype = C.c_uint64
+        lib.orc_rng_normal.argtypes = [C.c_void_p]
+        lib.orc_rng_normal.restype = C.c_double
+        lib.orc_rng_fill_normal.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+        lib.orc_rng_state_bytes.restype = C.c_size_t
+        _LIB = lib
+    return _LIB
+
+
+# ------------------------------------------------------------------------------------------------
+# Random input stream (include/xerus/tensor.h:212-220, misc/random.cpp:29-30, test.cpp:96-108)
+class Rng:
+    """std::mt19937_64 + std::normal_distribution<double> exactly as libstdc++ draws them."""
+
+    SEED = 0xBAADF00D  # src/xerus/test/test.cpp:105
+
+    def __init__(self, seed: int = SEED):
+        lib = _lib()
+        self._state = C.create_string_buffer(lib.orc_rng_state_bytes())
+        lib.orc_rng_seed(self._state, seed)
+
+    def normal(self, n: int) -> np.ndarray:
+        out = np.empty(int(n), dtype=np.float64)
+        if n:
+            _lib().orc_rng_fill_normal(self._state, out.ctypes.data, out.size)
+        return out
+
+
+def tensor_random(rng: Rng, dims: Sequence[int]) -> np.ndarray:
+    """Tensor::random: entries drawn in row-major order (tensor.h:212-220)."""
+    dims = tuple(int(d) for d in dims)
+    return rng.normal(int(np.prod(dims)) if dims else 1).reshape(dims)
+
+
+# ------------------------------------------------------------------------------------------------
+# Permutation (indexedTensor_tensor_evaluate.cpp:55-143) — bit-exact C restatement
+def reshuffle(base: np.ndarray, shuffle: Sequence[int]) -> np.ndarray:
+    base = np.ascontiguousarray(base, dtype=np.float64)
+    dims = base.shape
+    assert sorted(shuffle) == list(range(len(dims))), "shuffle must be a permutation"
+    out_dims = [0] * len(dims)
+    for i, s in enumerate(shuffle):
+        out_dims[s] = dims[i]
+    out = np.empty(out_dims, dtype=np.float64)
+    if base.ndim == 0:
+        out[()] = base[()]
+        return out
+    arr = lambda v: (C.c_size_t * len(v))(*v)
+    _lib().orc_reshuffle(out.ctypes.data, base.ctypes.data, len(dims), arr(dims), arr(list(shuffle)))
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Contraction (tensor.cpp:1252-1352 -> blasWrapper::matrix_matrix_product, blasLapackWrapper.cpp:149-195)
+def contract(lhs: np.ndarray, lhs_trans: bool, rhs: np.ndarray, rhs_trans: bool, num_modes: int,
+             alpha: float = 1.0) -> np.ndarray:
+    lo = lhs.ndim - num_modes
+    ro = rhs.ndim - num_modes
+    l_rem = lhs.shape[num_modes:] if lhs_trans else lhs.shape[:lo]
+    l_con = lhs.shape[:num_modes] if lhs_trans else lhs.shape[lo:]
+    r_rem = rhs.shape[:ro] if rhs_trans else rhs.shape[num_modes:]
+    r_con = rhs.shape[ro:] if rhs_trans else rhs.shape[:num_modes]
+    assert tuple(l_con) == tuple(r_con), (lhs.shape, rhs.shape, num_modes)
+    left, mid, right = int(np.prod(l_rem)), int(np.prod(l_con)), int(np.prod(r_rem))
+    A = lhs.reshape((mid, left) if lhs_trans else (left, mid))
+    B = rhs.reshape((right, mid) if rhs_trans else (mid, right))
+    Cm = alpha * ((A.T if lhs_trans else A) @ (B.T if rhs_trans else B))
+    return Cm.reshape(tuple(l_rem) + tuple(r_rem))
+
+
+def gemm(A, transA, B, transB, alpha=1.0):
+    return alpha * ((A.T if transA else A) @ (B.T if transB else B))
+
+
+# ------------------------------------------------------------------------------------------------
+# Factorisations (blasLapackWrapper.cpp:201-498)
+def qc(A: np.ndarray):
+    """Row-major QC with column pivoting (blasLapackWrapper.cpp:243-305)."""
+    m, n = A.shape
+    assert m > 0 and n > 0
+    max_rank = min(m, n)
+    qr_, jpvt, tau, _work, info = lapack.dgeqp3(np.asfortranarray(A, dtype=np.float64))
+    assert info == 0, "dgeqp3 failed"
+    # rank rule (:268-272): first k with |R_kk| < 16*eps*R_00 (R_00 NOT in abs)
+    rank = 1
+    while rank < max_rank and not (abs(qr_[rank, rank]) < 16 * DBL_EPSILON * qr_[0, 0]):
+        rank += 1
+    Cm = np.zeros((rank, n))
+    for col in range(n):  # (:280-285) un-permute the upper triangle
+        tgt = int(jpvt[col]) - 1
+        rows = min(rank, col + 1)
+        Cm[:rows, tgt] = qr_[:rows, col]
+    q, _w, info = lapack.dorgqr(qr_[:, :max_rank].copy(order="F"), tau[:max_rank])
+    assert info == 0
+    return np.ascontiguousarray(q[:, :rank]), Cm, rank
+
+
+def cq(A: np.ndarray):
+    """Row-major CQ: col-major dgeqp3 on A^T (blasLapackWrapper.cpp:317-371)."""
+    m, n = A.shape
+    Qt, Ct, rank = qc(np.ascontiguousarray(A.T))  # A^T = Qt Ct  ->  A = Ct^T Qt^T
+    return np.ascontiguousarray(Ct.T), np.ascontiguousarray(Qt.T), rank
+
+
+def qr(A: np.ndarray):
+    """Unpivoted QR, dgeqrf + dorgqr (blasLapackWrapper.cpp:388-431)."""
+    m, n = A.shape
+    k = min(m, n)
+    qr_, tau, _w, info = lapack.dgeqrf(np.asfortranarray(A, dtype=np.float64))
+    assert info == 0
+    R = np.triu(qr_[:k, :])
+    q, _w, info = lapack.dorgqr(qr_[:, :k].copy(order="F"), tau[:k])
+    return np.ascontiguousarray(q), np.ascontiguousarray(R)
+
+
+def rq(A: np.ndarray):
+    """Unpivoted RQ (blasLapackWrapper.cpp:445-498): A = R Q, R m x k, Q k x n."""
+    Qt, Rt = qr(np.ascontiguousarray(A.T))  # A^T = Qt Rt -> A = Rt^T Qt^T
+    return np.ascontiguousarray(Rt.T), np.ascontiguousarray(Qt.T)
+
+
+def svd(A: np.ndarray):
+    """Thin SVD via dgesdd 'S' (blasLapackWrapper.cpp:210-232)."""
+    u, s, vt, info = lapack.dgesdd(np.asfortranarray(A, dtype=np.float64), compute_uv=1, full_matrices=0)
+    assert info == 0, "dgesdd failed"
+    return np.ascontiguousarray(u), s.copy(), np.ascontiguousarray(vt)
+
+
+def svd_rank(s: np.ndarray, max_rank: int, eps: float) -> int:
+    """Rank cut of calculate_svd (tensor.cpp:1462-1474)."""
+    rank = len(s)
+    if max_rank != 0:
+        rank = min(rank, max_rank)
+    for j in range(1, rank):
+        if s[j] <= eps * s[0]:
+            return j
+    return rank
+
+
+# ------------------------------------------------------------------------------------------------
+# TT format (ttNetwork.cpp / tensorNetwork.cpp). Core k has dims (r_k, n_k, r_{k+1}), r_0 = r_d = 1.
+def reduce_to_maximal_ranks(ranks: Sequence[int], dims: Sequence[int]) -> List[int]:
+    """ttNetwork.cpp:370-402 (TTTensor, N = 1)."""
+    ranks = list(ranks)
+    d = len(dims)
+    cur = 1
+    for i in range(d - 1):
+        cur *= dims[i]
+        if cur < ranks[i]:
+            ranks[i] = cur
+        else:
+            cur = ranks[i]
+    cur = 1
+    for i in range(1, d):
+        cur *= dims[d - i]
+        if cur < ranks[d - i - 1]:
+            ranks[d - i - 1] = cur
+        else:
+            cur = ranks[d - i - 1]
+    return ranks
+
+
+@dataclass
+class TT:
+    cores: List[np.ndarray]
+    canonicalized: bool = False
+    core_position: int = 0
+
+    @property
+    def order(self) -> int:
+        return len(self.cores)
+
+    @property
+    def dims(self) -> List[int]:
+        return [c.shape[1] for c in self.cores]
+
+    @property
+    def ranks(self) -> List[int]:
+        return [c.shape[2] for c in self.cores[:-1]]
+
+    def copy(self) -> "TT":
+        return TT([c.copy() for c in self.cores], self.canonicalized, self.core_position)
+
+    @staticmethod
+    def random(dims: Sequence[int], ranks: Sequence[int], rng: Rng) -> "TT":
+        """TTNetwork::random (include/xerus/ttNetwork.h:129-157): raw N(0,1) cores, then move_core(0)."""
+        tt = TT.random_raw(dims, ranks, rng)
+        tt.move_core(0)
+        return tt
+
+    @staticmethod
+    def random_raw(dims: Sequence[int], ranks: Sequence[int], rng: Rng) -> "TT":
+        target = reduce_to_maximal_ranks(ranks, dims)
+        d = len(dims)
+        cores = []
+        for i in range(d):
+            left = 1 if i == 0 else target[i - 1]
+            right = 1 if i == d - 1 else target[i]
+            cores.append(tensor_random(rng, (left, dims[i], right)))
+        return TT(cores)
+
+    # ---- transfer_core (tensorNetwork.cpp:821-909) restricted to TT neighbours
+    def transfer_core(self, frm: int, to: int, allow_rank_reduction: bool = True):
+        X = self.cores[frm]
+        a, n, b = X.shape
+        if to == frm + 1:  # posA = last mode -> QC / QR (:842-848), posB = 0 -> R * to (:873)
+            M = X.reshape(a * n, b)
+            if allow_rank_reduction:
+                Q, R, rank = qc(M)
+            else:
+                Q, R = qr(M)
+                rank = Q.shape[1]
+            self.cores[frm] = Q.reshape(a, n, rank)
+            nxt = self.cores[to]
+            self.cores[to] = (R @ nxt.reshape(nxt.shape[0], -1)).reshape(rank, nxt.shape[1], nxt.shape[2])
+        elif to == frm - 1:  # posA = 0 -> CQ / RQ (:834-841), posB = last -> to * R (:875-876)
+            M = X.reshape(a, n * b)
+            if allow_rank_reduction:
+                R, Q, rank = cq(M)
+            else:
+                R, Q = rq(M)
+                rank = Q.shape[0]
+            self.cores[frm] = Q.reshape(rank, n, b)
+            prv = self.cores[to]
+            self.cores[to] = (prv.reshape(-1, prv.shape[2]) @ R).reshape(prv.shape[0], prv.shape[1], rank)
+        else:
+            raise ValueError("not neighbours")
+
+    def exceeds_maximal_ranks(self) -> bool:
+        return self.ranks != reduce_to_maximal_ranks(self.ranks, self.dims)
+
+    def move_core(self, position: int, keep_rank: bool = False):
+        """TTNetwork::move_core (ttNetwork.cpp:582-628)."""
+        d = self.order
+        assert 0 <= position < d
+        if self.canonicalized:
+            for k in range(self.core_position, position):
+                self.transfer_core(k, k + 1, not keep_rank)
+            for k in range(self.core_position, position, -1):
+                self.transfer_core(k, k - 1, not keep_rank)
+        else:
+            for k in range(0, position):
+                self.transfer_core(k, k + 1, not keep_rank)
+            for k in range(d - 1, position, -1):
+                self.transfer_core(k, k - 1, not keep_rank)
+        while self.exceeds_maximal_ranks():
+            for k in range(position, 0, -1):
+                self.transfer_core(k, k - 1, not keep_rank)
+            for k in range(0, d - 1):
+                self.transfer_core(k, k + 1, not keep_rank)
+            for k in range(d - 1, position, -1):
+                self.transfer_core(k, k - 1, not keep_rank)
+        self.canonicalized = True
+        self.core_position = position
+
+    # ---- round_edge (tensorNetwork.cpp:678-818) for TT: from = right core (fromPos = 0, transFrom),
+    #      to = left core (toPos = last, transTo)
+    def round_edge(self, frm: int, to: int, max_rank: int, eps: float):
+        F = self.cores[frm]          # (b, n, c)
+        T = self.cores[to]           # (a, n', b)
+        b = F.shape[0]
+        if 5 * F.size * T.size >= 6 * b ** 4:   # (:745)
+            coreA, Qf, _ = cq(F.reshape(b, -1))           # F = coreA * Qf  (:749)
+            Qt, coreB, _ = qc(T.reshape(-1, b))           # T = Qt * coreB  (:755)
+            X = coreA.T @ coreB.T                         # contract(X, coreA, true, coreB, true, 1) (:761)
+            U, S, Vt = svd(X)                             # (:764)
+            k = svd_rank(S, max_rank, eps)
+            U, S, Vt = U[:, :k], S[:k], Vt[:k, :]
+            coreB = S[:, None] * Vt                       # (:769)
+            self.cores[frm] = (U.T @ Qf).reshape(k, F.shape[1], F.shape[2])           # (:773)
+            self.cores[to] = (Qt @ coreB.T).reshape(T.shape[0], T.shape[1], k)        # (:779)
+        else:
+            X = F.reshape(b, -1).T @ T.reshape(-1, b).T   # (n c) x (a n') (:783)
+            U, S, Vt = svd(X)
+            k = svd_rank(S, max_rank, eps)
+            U, S, Vt = U[:, :k], S[:k], Vt[:k, :]
+            self.cores[to] = (Vt.T * S[None, :]).reshape(T.shape[0], T.shape[1], k)   # (:790-791)
+            self.cores[frm] = np.ascontiguousarray(U.T).reshape(k, F.shape[1], F.shape[2])  # (:797-802)
+
+    def round(self, max_ranks, eps: float = EPSILON):
+        """TTNetwork::round (ttNetwork.cpp:644-665); an int max_ranks means round(size_t) (:669-672)."""
+        d = self.order
+        if isinstance(max_ranks, (int, np.integer)):
+            max_ranks = [int(max_ranks)] * (d - 1)
+        init_canon, init_pos = self.canonicalized, self.core_position
+        self.move_core(d - 1)
+        for i in range(d - 1):
+            self.round_edge(d - 1 - i, d - 2 - i, max_ranks[d - 2 - i], eps)
+        self.core_position = 0
+        self.canonicalized = True
+        if init_canon:
+            self.move_core(init_pos)
+
+    # ---- evaluation
+    def full(self) -> np.ndarray:
+        res = self.cores[0]
+        for c in self.cores[1:]:
+            res = np.tensordot(res, c, axes=([res.ndim - 1], [0]))
+        return res.reshape(self.dims)
+
+    def frob_norm(self) -> float:
+        """ttNetwork.cpp:782-789."""
+        if self.canonicalized:
+            return float(np.linalg.norm(self.cores[self.core_position]))
+        return float(np.sqrt(max(0.0, dot(self, self))))
+
+
+def dot(x: TT, y: TT) -> float:
+    """<x,y> as a left-to-right zipper (the order the reference's heuristics pick)."""
+    E = np.ones((1, 1))
+    for X, Y in zip(x.cores, y.cores):
+        rx, n, rx2 = X.shape
+        ry, _, ry2 = Y.shape
+        T = E.T @ X.reshape(rx, n * rx2)                     # ry x (n rx2)
+        E = T.reshape(ry * n, rx2).T @ Y.reshape(ry * n, ry2)  # rx2 x ry2
+    return float(E[0, 0])
+
+
+def tt_flops_dot(x: TT, y: TT) -> float:
+    f = 0.0
+    for X, Y in zip(x.cores, y.cores):
+        rx, n, rx2 = X.shape
+        ry, _, ry2 = Y.shape
+        f += 2.0 * rx * ry * n * rx2 + 2.0 * ry * n * rx2 * ry2
+    return f
+
+
+def tt_add(x: TT, y: TT) -> TT:
+    """TTNetwork::operator+= (ttNetwork.cpp:797-847): block-diagonal core assembly, not canonical."""
+    d = x.order
+    assert x.dims == y.dims
+    cores = []
+    for k, (X, Y) in enumerate(zip(x.cores, y.cores)):
+        if d == 1:
+            cores.append(X + Y)
+            continue
+        a1, n, b1 = X.shape
+        a2, _, b2 = Y.shape
+        if k == 0:
+            cores.append(np.concatenate([X, Y], axis=2))
+        elif k == d - 1:
+            cores.append(np.concatenate([X, Y], axis=0))
+        else:
+            Z = np.zeros((a1 + a2, n, b1 + b2))
+            Z[:a1, :, :b1] = X
+            Z[a1:, :, b1:] = Y
+            cores.append(Z)
+    return TT(cores)

@@ -1,0 +1,93 @@
+"""GPU parity of the level-1/3 and permutation kernels against the oracle (through the C-ABI)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+PERMS = [
+    ((64, 64, 64), (0, 2, 1)),            # cfg1's C reshuffle
+    ((64, 64, 64), (2, 1, 0)),
+    ((256, 20, 256), (1, 0, 2)),          # contiguous block kept
+    ((256, 20, 256), (2, 1, 0)),
+    ((1, 1, 256, 20, 256), (0, 1, 3, 4, 2)),  # cfg4 zipper reshuffle
+    ((1, 1, 256, 256), (0, 1, 3, 2)),
+    ((1024, 1024), (1, 0)),
+    ((20, 20, 20, 20, 20, 20), (5, 4, 3, 2, 1, 0)),
+    ((3, 5, 7, 11), (2, 0, 3, 1)),
+    ((2, 3, 4, 5, 6), (4, 2, 0, 1, 3)),
+    ((33, 65), (1, 0)),                   # ragged tiles
+    ((1, 7, 1), (2, 1, 0)),
+    ((5,), (0,)),
+    ((0, 4), (1, 0)),                     # empty
+    ((4, 1, 3, 1, 2), (3, 0, 4, 1, 2)),
+]
+
+
+@pytest.mark.parametrize("dims,shuffle", PERMS)
+def test_permute_bit_exact(handle, ref, dims, shuffle):
+    a = np.random.default_rng(11).standard_normal(dims)
+    d = handle.array(a)
+    out = handle.reshuffle(d, shuffle).numpy()
+    expect = ref.reshuffle(a, shuffle)
+    assert out.shape == expect.shape
+    assert np.array_equal(out, expect)
+
+
+def test_permute_rejects_bad_shuffle(handle):
+    from xerus_amd.capi import XrsError
+
+    d = handle.array(np.zeros((2, 3)))
+    o = handle.empty((3, 2))
+    with pytest.raises(XrsError):
+        handle.permute(o, d, (2, 3), (0, 0))
+
+
+GEMMS = [
+    (64, 64, 4096, False, False),    # cfg1 GEMM
+    (1024, 1024, 1024, False, False),  # cfg2
+    (256, 5120, 256, True, False),   # TT zipper step 1
+    (256, 256, 5120, True, False),   # TT zipper step 2 (split-K)
+    (5120, 256, 256, False, False),  # R * core
+    (256, 256, 5120, False, True),   # Gram of a wide core
+    (128, 2560, 128, True, True),
+    (1, 37, 19, False, False), (37, 1, 19, True, False), (13, 17, 1, False, True),
+    (100, 3, 7, True, True), (129, 131, 67, False, False), (65, 63, 2000, True, True),
+]
+
+
+@pytest.mark.parametrize("M,N,K,ta,tb", GEMMS)
+def test_gemm_fp64(handle, ref, M, N, K, ta, tb):
+    rng = np.random.default_rng(M * 7 + N * 3 + K)
+    A = rng.standard_normal((K, M) if ta else (M, K))
+    B = rng.standard_normal((N, K) if tb else (K, N))
+    alpha = -1.75
+    dA, dB = handle.array(A), handle.array(B)
+    Cd = handle.matmul(dA, ta, dB, tb, alpha).numpy()
+    expect = ref.gemm(A, ta, B, tb, alpha)
+    err = np.linalg.norm(Cd - expect) / max(np.linalg.norm(expect), 1e-300)
+    assert err <= 1e-13, err  # fp64 MFMA: relative Frobenius error at rounding level
+
+
+def test_gemm_zero_k(handle):
+    dA, dB = handle.array(np.zeros((3, 0))), handle.array(np.zeros((0, 4)))
+    out = handle.empty((3, 4))
+    handle.gemm(out, 3, 4, 1.0, dA, 1, False, 0, dB, 4, False)
+    assert np.array_equal(out.numpy(), np.zeros((3, 4)))
+
+
+def test_level1(handle):
+    rng = np.random.default_rng(5)
+    x, y = rng.standard_normal(100003), rng.standard_normal(100003)
+    dx, dy = handle.array(x), handle.array(y)
+    assert np.isclose(handle.nrm2(dx), np.linalg.norm(x), rtol=1e-14)
+    assert np.isclose(handle.dot(dx, dy), x @ y, rtol=1e-12)
+    assert np.isclose(handle.asum(dx), np.abs(x).sum(), rtol=1e-14)
+    handle.scal(dx, 2.5)
+    assert np.allclose(dx.numpy(), 2.5 * x, rtol=0, atol=0)
+    handle.axpy(dy, -0.5, dx)
+    assert np.allclose(dy.numpy(), y - 0.5 * (2.5 * x), rtol=1e-15, atol=1e-15)
+    M = rng.standard_normal((37, 53))
+    s = rng.standard_normal(37)
+    dM = handle.array(M)
+    handle.scale_rows(dM, handle.array(s))
+    assert np.array_equal(dM.numpy(), M * s[:, None])

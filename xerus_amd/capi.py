@@ -1,0 +1,284 @@
+"""ctypes binding of the C-ABI in include/xerus_amd.h (libxerus_amd.so).
+
+This is the Python side of the drop-in boundary: every call goes straight to the HIP kernels in
+libxerus_amd.so. There is deliberately no CPU fallback — if the library (or a GPU) is missing,
+loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libxerus_amd.so")
+
+_SZ = C.c_size_t
+_DP = C.c_void_p
+
+# (name, restype, argtypes) for every symbol declared in include/xerus_amd.h
+SIGNATURES = {
+    "xrs_create": (C.c_int, [C.POINTER(_DP), C.c_int]),
+    "xrs_destroy": (C.c_int, [_DP]),
+    "xrs_set_stream": (C.c_int, [_DP, _DP]),
+    "xrs_get_stream": (_DP, [_DP]),
+    "xrs_synchronize": (C.c_int, [_DP]),
+    "xrs_last_error": (C.c_char_p, []),
+    "xrs_version": (C.c_char_p, []),
+    "xrs_malloc": (C.c_int, [_DP, C.POINTER(_DP), _SZ]),
+    "xrs_free": (C.c_int, [_DP, _DP]),
+    "xrs_pool_bytes": (_SZ, [_DP]),
+    "xrs_upload": (C.c_int, [_DP, _DP, _DP, _SZ]),
+    "xrs_download": (C.c_int, [_DP, _DP, _DP, _SZ]),
+    "xrs_memset_zero": (C.c_int, [_DP, _DP, _SZ]),
+    "xrs_copy": (C.c_int, [_DP, _DP, _DP, _SZ]),
+    "xrs_nrm2": (C.c_int, [_DP, C.POINTER(C.c_double), _DP, _SZ]),
+    "xrs_dot": (C.c_int, [_DP, C.POINTER(C.c_double), _DP, _DP, _SZ]),
+    "xrs_asum": (C.c_int, [_DP, C.POINTER(C.c_double), _DP, _SZ]),
+    "xrs_scal": (C.c_int, [_DP, _DP, C.c_double, _SZ]),
+    "xrs_axpy": (C.c_int, [_DP, _DP, C.c_double, _DP, _SZ]),
+    "xrs_scale_rows": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ]),
+    "xrs_gemm": (C.c_int, [_DP, _DP, _SZ, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
+    "xrs_permute": (C.c_int, [_DP, _DP, _DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "xrs_qc": (C.c_int, [_DP, _DP, _DP, C.POINTER(_SZ), _DP, _SZ, _SZ]),
+    "xrs_cq": (C.c_int, [_DP, _DP, _DP, C.POINTER(_SZ), _DP, _SZ, _SZ]),
+    "xrs_qr": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
+    "xrs_rq": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
+    "xrs_svd": (C.c_int, [_DP, _DP, _DP, _DP, _DP, _SZ, _SZ]),
+    "xrs_tt_move_core": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ, _SZ, C.c_int]),
+    "xrs_tt_round": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ,
+                               C.POINTER(_SZ), C.c_double]),
+    "xrs_tt_dot": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
+                             C.POINTER(_SZ), C.POINTER(_DP)]),
+    "xrs_prof_begin": (C.c_int, [_DP, C.c_uint32]),
+    "xrs_prof_end": (C.c_int, [_DP, C.POINTER(_SZ), C.POINTER(C.c_double), C.POINTER(C.c_double),
+                               C.POINTER(C.c_double)]),
+}
+
+KFAM_GEMM, KFAM_PERMUTE, KFAM_QR, KFAM_SVD, KFAM_ELEMWISE = 1, 2, 4, 8, 16
+
+_lib = None
+
+
+class XrsError(RuntimeError):
+    """A non-zero status from the C-ABI (the reference raises xerus::misc::generic_error)."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        super().__init__(f"{fn} failed with status {code}: {msg}")
+        self.code = code
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load libxerus_amd.so and attach the signatures. Raises if the library is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(f"{p} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = C.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(fn: str, status: int):
+    if status != 0:
+        raise XrsError(fn, status, load().xrs_last_error().decode())
+
+
+def _arr(vals: Sequence[int]):
+    return (_SZ * len(vals))(*[int(v) for v in vals])
+
+
+class Handle:
+    """One HIP stream + caching allocator (xrs_handle_t)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.h = _DP()
+        _check("xrs_create", self.lib.xrs_create(C.byref(self.h), device))
+
+    def close(self):
+        if self.h:
+            _check("xrs_destroy", self.lib.xrs_destroy(self.h))
+            self.h = _DP()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- memory
+    def malloc(self, nbytes: int) -> int:
+        p = _DP()
+        _check("xrs_malloc", self.lib.xrs_malloc(self.h, C.byref(p), nbytes))
+        return p.value or 0
+
+    def free(self, ptr: int):
+        _check("xrs_free", self.lib.xrs_free(self.h, _DP(ptr)))
+
+    def synchronize(self):
+        _check("xrs_synchronize", self.lib.xrs_synchronize(self.h))
+
+    def set_stream(self, stream_ptr: int | None):
+        _check("xrs_set_stream", self.lib.xrs_set_stream(self.h, _DP(stream_ptr or 0)))
+
+    def stream(self) -> int:
+        return self.lib.xrs_get_stream(self.h) or 0
+
+    def array(self, a: np.ndarray) -> "DeviceArray":
+        return DeviceArray.from_host(self, a)
+
+    def empty(self, shape) -> "DeviceArray":
+        return DeviceArray(self, tuple(int(s) for s in shape))
+
+    def zeros(self, shape) -> "DeviceArray":
+        d = DeviceArray(self, tuple(int(s) for s in shape))
+        _check("xrs_memset_zero", self.lib.xrs_memset_zero(self.h, _DP(d.ptr), d.size))
+        return d
+
+    # ---- kernels
+    def gemm(self, C_: "DeviceArray", M, N, alpha, A: "DeviceArray", lda, transA, K, B: "DeviceArray", ldb, transB):
+        _check("xrs_gemm", self.lib.xrs_gemm(self.h, _DP(C_.ptr), M, N, alpha, _DP(A.ptr), lda, int(transA), K,
+                                            _DP(B.ptr), ldb, int(transB)))
+
+    def matmul(self, A: "DeviceArray", transA: bool, B: "DeviceArray", transB: bool, alpha: float = 1.0):
+        """Row-major C = alpha*op(A)*op(B) with the reference's inline-overload ld convention."""
+        am, ak = (A.shape[1], A.shape[0]) if transA else (A.shape[0], A.shape[1])
+        bk, bn = (B.shape[1], B.shape[0]) if transB else (B.shape[0], B.shape[1])
+        assert ak == bk, (A.shape, B.shape)
+        out = self.empty((am, bn))
+        self.gemm(out, am, bn, alpha, A, A.shape[1], transA, ak, B, B.shape[1], transB)
+        return out
+
+    def permute(self, out: "DeviceArray", inp: "DeviceArray", dims, shuffle):
+        _check("xrs_permute", self.lib.xrs_permute(self.h, _DP(out.ptr), _DP(inp.ptr), len(dims), _arr(dims),
+                                                  _arr(shuffle)))
+
+    def reshuffle(self, inp: "DeviceArray", shuffle):
+        dims = inp.shape
+        out_dims = [0] * len(dims)
+        for i, s in enumerate(shuffle):
+            out_dims[s] = dims[i]
+        out = self.empty(tuple(out_dims))
+        self.permute(out, inp, dims, shuffle)
+        return out
+
+    def nrm2(self, x: "DeviceArray") -> float:
+        r = C.c_double()
+        _check("xrs_nrm2", self.lib.xrs_nrm2(self.h, C.byref(r), _DP(x.ptr), x.size))
+        return r.value
+
+    def dot(self, x: "DeviceArray", y: "DeviceArray") -> float:
+        r = C.c_double()
+        _check("xrs_dot", self.lib.xrs_dot(self.h, C.byref(r), _DP(x.ptr), _DP(y.ptr), x.size))
+        return r.value
+
+    def asum(self, x: "DeviceArray") -> float:
+        r = C.c_double()
+        _check("xrs_asum", self.lib.xrs_asum(self.h, C.byref(r), _DP(x.ptr), x.size))
+        return r.value
+
+    def scal(self, x: "DeviceArray", alpha: float):
+        _check("xrs_scal", self.lib.xrs_scal(self.h, _DP(x.ptr), alpha, x.size))
+
+    def axpy(self, y: "DeviceArray", alpha: float, x: "DeviceArray"):
+        _check("xrs_axpy", self.lib.xrs_axpy(self.h, _DP(y.ptr), alpha, _DP(x.ptr), x.size))
+
+    def scale_rows(self, X: "DeviceArray", s: "DeviceArray"):
+        _check("xrs_scale_rows", self.lib.xrs_scale_rows(self.h, _DP(X.ptr), _DP(s.ptr), X.shape[0], X.size // max(1, X.shape[0])))
+
+    def qc(self, A: "DeviceArray"):
+        m, n = A.shape
+        k = min(m, n)
+        Q, Cm = self.empty((m, k)), self.empty((k, n))
+        r = _SZ()
+        _check("xrs_qc", self.lib.xrs_qc(self.h, _DP(Q.ptr), _DP(Cm.ptr), C.byref(r), _DP(A.ptr), m, n))
+        rank = r.value
+        Q.shape, Cm.shape = (m, rank), (rank, n)
+        return Q, Cm, rank
+
+    def cq(self, A: "DeviceArray"):
+        m, n = A.shape
+        k = min(m, n)
+        Cm, Q = self.empty((m, k)), self.empty((k, n))
+        r = _SZ()
+        _check("xrs_cq", self.lib.xrs_cq(self.h, _DP(Cm.ptr), _DP(Q.ptr), C.byref(r), _DP(A.ptr), m, n))
+        rank = r.value
+        Cm.shape, Q.shape = (m, rank), (rank, n)
+        return Cm, Q, rank
+
+    def qr(self, A: "DeviceArray"):
+        m, n = A.shape
+        k = min(m, n)
+        Q, R = self.empty((m, k)), self.empty((k, n))
+        _check("xrs_qr", self.lib.xrs_qr(self.h, _DP(Q.ptr), _DP(R.ptr), _DP(A.ptr), m, n))
+        return Q, R
+
+    def rq(self, A: "DeviceArray"):
+        m, n = A.shape
+        k = min(m, n)
+        R, Q = self.empty((m, k)), self.empty((k, n))
+        _check("xrs_rq", self.lib.xrs_rq(self.h, _DP(R.ptr), _DP(Q.ptr), _DP(A.ptr), m, n))
+        return R, Q
+
+    def svd(self, A: "DeviceArray"):
+        m, n = A.shape
+        k = min(m, n)
+        U, S, Vt = self.empty((m, k)), self.empty((k,)), self.empty((k, n))
+        _check("xrs_svd", self.lib.xrs_svd(self.h, _DP(U.ptr), _DP(S.ptr), _DP(Vt.ptr), _DP(A.ptr), m, n))
+        return U, S, Vt
+
+    # ---- profiling
+    def prof_begin(self, mask: int):
+        _check("xrs_prof_begin", self.lib.xrs_prof_begin(self.h, mask))
+
+    def prof_end(self):
+        n, ms, fl, by = _SZ(), C.c_double(), C.c_double(), C.c_double()
+        _check("xrs_prof_end", self.lib.xrs_prof_end(self.h, C.byref(n), C.byref(ms), C.byref(fl), C.byref(by)))
+        return {"launches": n.value, "ms": ms.value, "flops": fl.value, "bytes": by.value}
+
+
+class DeviceArray:
+    """A row-major float64 array in the handle's device pool."""
+
+    def __init__(self, handle: Handle, shape: tuple, ptr: int | None = None, owned: bool = True):
+        self.handle = handle
+        self.shape = tuple(shape)
+        self.size = int(np.prod(self.shape)) if self.shape else 1
+        self.owned = owned and ptr is None
+        self.ptr = ptr if ptr is not None else (handle.malloc(max(8, self.size * 8)))
+
+    @classmethod
+    def from_host(cls, handle: Handle, a: np.ndarray) -> "DeviceArray":
+        a = np.ascontiguousarray(a, dtype=np.float64)
+        d = cls(handle, a.shape)
+        if a.size:
+            _check("xrs_upload", handle.lib.xrs_upload(handle.h, _DP(d.ptr), a.ctypes.data_as(_DP), a.size))
+        return d
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, dtype=np.float64)
+        if self.size:
+            _check("xrs_download", self.handle.lib.xrs_download(self.handle.h, out.ctypes.data_as(_DP), _DP(self.ptr),
+                                                               self.size))
+        return out
+
+    def free(self):
+        if self.owned and self.ptr:
+            self.handle.free(self.ptr)
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

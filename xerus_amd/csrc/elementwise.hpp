@@ -1,0 +1,24 @@
+// Internal entry points shared between the kernel translation units and the TT drivers.
+#pragma once
+#include <algorithm>
+
+#include "runtime.hpp"
+
+namespace xrs {
+
+// level 1 / elementwise (elementwise.hip)
+void reduce_to_device(xrs_handle_t h, int mode, const double* x, const double* y, size_t n, double* out_dev);
+double reduce_to_host(xrs_handle_t h, int mode, const double* x, const double* y, size_t n);
+void scal(xrs_handle_t h, double* x, double alpha, size_t n);
+void axpy(xrs_handle_t h, double* y, double alpha, const double* x, size_t n);
+void scale_rows(xrs_handle_t h, double* X, const double* s, size_t m, size_t n);
+void scale_cols(xrs_handle_t h, double* X, const double* s, size_t m, size_t n);
+
+// gemm.hip
+void gemm(xrs_handle_t h, double* C, size_t M, size_t N, double alpha, const double* A, size_t lda, bool ta, size_t K,
+          const double* B, size_t ldb, bool tb);
+
+// permute.hip
+void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const size_t* dims, const size_t* shuffle);
+
+}  // namespace xrs

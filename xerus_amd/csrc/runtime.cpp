@@ -1,0 +1,236 @@
+// Handle, stream, caching allocator, profiler and the runtime part of the C-ABI.
+#include "runtime.hpp"
+
+#include <cstring>
+
+namespace xrs {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+Pool::~Pool() { trim(); }
+
+static size_t round_size(size_t bytes) {
+    if (bytes <= (1u << 20)) {
+        size_t s = 256;
+        while (s < bytes) s <<= 1;
+        return s;
+    }
+    return (bytes + (1u << 20) - 1) & ~size_t((1u << 20) - 1);
+}
+
+void* Pool::alloc(size_t bytes) {
+    const size_t sz = round_size(bytes);
+    auto it = free_.lower_bound(sz);
+    if (it != free_.end() && it->first <= sz + sz / 4) {
+        void* p = it->second;
+        live_[p] = it->first;
+        free_.erase(it);
+        return p;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, sz);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        // give cached blocks back and retry once
+        trim();
+        e = hipMalloc(&p, sz);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            throw Error{XRS_ENOMEM, "device allocation of " + std::to_string(sz) + " bytes failed"};
+        }
+    }
+    live_[p] = sz;
+    held_ += sz;
+    return p;
+}
+
+void Pool::release(void* p) {
+    auto it = live_.find(p);
+    if (it == live_.end()) throw Error{XRS_EINVAL, "xrs_free: pointer not owned by this handle"};
+    free_.emplace(it->second, p);
+    live_.erase(it);
+}
+
+void Pool::trim() {
+    if (free_.empty()) return;
+    (void)hipDeviceSynchronize();
+    for (auto& kv : free_) {
+        (void)hipFree(kv.second);
+        held_ -= kv.first;
+    }
+    free_.clear();
+}
+
+KernelTimer::KernelTimer(xrs_handle_t h, uint32_t family, double flops, double bytes)
+    : h_(h), on_((h->prof_mask & family) != 0) {
+    if (!on_) return;
+    auto get = [&]() {
+        hipEvent_t e;
+        if (!h_->event_cache.empty()) {
+            e = h_->event_cache.back();
+            h_->event_cache.pop_back();
+        } else {
+            XRS_HIP(hipEventCreate(&e));
+        }
+        return e;
+    };
+    rec_.start = get();
+    rec_.stop = get();
+    rec_.flops = flops;
+    rec_.bytes = bytes;
+    XRS_HIP(hipEventRecord(rec_.start, h_->stream));
+}
+
+KernelTimer::~KernelTimer() {
+    if (!on_) return;
+    (void)hipEventRecord(rec_.stop, h_->stream);
+    h_->prof.push_back(rec_);
+}
+
+void check_launch(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw Error{XRS_EHIP, std::string(what) + ": " + hipGetErrorString(e)};
+}
+
+}  // namespace xrs
+
+using namespace xrs;
+
+extern "C" {
+
+const char* xrs_last_error(void) { return g_last_error.c_str(); }
+const char* xrs_version(void) { return "xerus_amd 0.1 (gfx950)"; }
+
+int xrs_create(xrs_handle_t* handle, int device) {
+    return guarded([&] {
+        XRS_REQUIRE(handle != nullptr, "null handle pointer");
+        int count = 0;
+        XRS_HIP(hipGetDeviceCount(&count));
+        XRS_REQUIRE(device >= 0 && device < count, "device index out of range");
+        XRS_HIP(hipSetDevice(device));
+        auto* h = new xrs_handle_s();
+        h->device = device;
+        XRS_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
+        h->stream = h->own_stream;
+        h->pool = new Pool(device);
+        XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
+        XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
+        *handle = h;
+    });
+}
+
+int xrs_destroy(xrs_handle_t h) {
+    return guarded([&] {
+        if (!h) return;
+        (void)hipSetDevice(h->device);
+        (void)hipStreamSynchronize(h->stream);
+        for (auto& r : h->prof) {
+            (void)hipEventDestroy(r.start);
+            (void)hipEventDestroy(r.stop);
+        }
+        for (auto e : h->event_cache) (void)hipEventDestroy(e);
+        delete h->pool;
+        (void)hipHostFree(h->host_scratch);
+        (void)hipFree(h->dev_scratch);
+        if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+        delete h;
+    });
+}
+
+int xrs_set_stream(xrs_handle_t h, void* s) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        h->stream = s ? static_cast<hipStream_t>(s) : h->own_stream;
+    });
+}
+
+void* xrs_get_stream(xrs_handle_t h) { return h ? static_cast<void*>(h->stream) : nullptr; }
+
+int xrs_synchronize(xrs_handle_t h) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        XRS_HIP(hipStreamSynchronize(h->stream));
+    });
+}
+
+int xrs_malloc(xrs_handle_t h, void** ptr, size_t bytes) {
+    return guarded([&] {
+        XRS_REQUIRE(h && ptr, "null argument");
+        *ptr = bytes ? h->pool->alloc(bytes) : nullptr;
+    });
+}
+
+int xrs_free(xrs_handle_t h, void* ptr) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        if (ptr) h->pool->release(ptr);
+    });
+}
+
+size_t xrs_pool_bytes(xrs_handle_t h) { return h ? h->pool->held_bytes() : 0; }
+
+int xrs_upload(xrs_handle_t h, double* dst, const double* src, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && (n == 0 || (dst && src)), "null argument");
+        if (n == 0) return;
+        XRS_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+    });
+}
+
+int xrs_download(xrs_handle_t h, double* dst, const double* src, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && (n == 0 || (dst && src)), "null argument");
+        if (n == 0) return;
+        XRS_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+    });
+}
+
+int xrs_memset_zero(xrs_handle_t h, double* dst, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && (n == 0 || dst), "null argument");
+        if (n) XRS_HIP(hipMemsetAsync(dst, 0, n * sizeof(double), h->stream));
+    });
+}
+
+int xrs_copy(xrs_handle_t h, double* dst, const double* src, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && (n == 0 || (dst && src)), "null argument");
+        if (n) XRS_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    });
+}
+
+int xrs_prof_begin(xrs_handle_t h, uint32_t mask) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        h->prof_mask = mask;
+    });
+}
+
+int xrs_prof_end(xrs_handle_t h, size_t* launches, double* total_ms, double* flops, double* bytes) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        h->prof_mask = 0;
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        double ms = 0, f = 0, b = 0;
+        for (auto& r : h->prof) {
+            float t = 0;
+            XRS_HIP(hipEventElapsedTime(&t, r.start, r.stop));
+            ms += t;
+            f += r.flops;
+            b += r.bytes;
+            h->event_cache.push_back(r.start);
+            h->event_cache.push_back(r.stop);
+        }
+        if (launches) *launches = h->prof.size();
+        if (total_ms) *total_ms = ms;
+        if (flops) *flops = f;
+        if (bytes) *bytes = b;
+        h->prof.clear();
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,137 @@
+// Internal runtime of libxerus_amd: handle (stream + caching allocator + profiler), error plumbing.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/xerus_amd.h"
+
+namespace xrs {
+
+// ---------------------------------------------------------------------------------------------
+// Errors: the C-ABI returns int status codes; internally we throw and convert at the boundary.
+struct Error {
+    int code;
+    std::string msg;
+};
+
+void set_last_error(const std::string& msg);
+
+#define XRS_REQUIRE(cond, msg)                                                          \
+    do {                                                                                \
+        if (!(cond)) {                                                                  \
+            throw ::xrs::Error{XRS_EINVAL, std::string(__func__) + ": " + (msg)};      \
+        }                                                                               \
+    } while (0)
+
+#define XRS_HIP(call)                                                                   \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            throw ::xrs::Error{XRS_EHIP, std::string(#call) + ": " + hipGetErrorString(e_)}; \
+        }                                                                               \
+    } while (0)
+
+// Run `body` and translate exceptions into C status codes.
+template <class F>
+int guarded(F&& body) {
+    try {
+        body();
+        return XRS_OK;
+    } catch (const Error& e) {
+        set_last_error(e.msg);
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return XRS_EINVAL;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Stream-ordered caching allocator. All work of a handle runs on one stream, so a block freed on
+// the host may be handed to a later launch on the same stream immediately.
+class Pool {
+   public:
+    explicit Pool(int device) : device_(device) {}
+    ~Pool();
+    void* alloc(size_t bytes);
+    void release(void* p);
+    size_t held_bytes() const { return held_; }
+    void trim();
+
+   private:
+    int device_;
+    std::multimap<size_t, void*> free_;
+    std::unordered_map<void*, size_t> live_;
+    size_t held_ = 0;
+};
+
+struct ProfRecord {
+    hipEvent_t start, stop;
+    double flops, bytes;
+};
+
+}  // namespace xrs
+
+struct xrs_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipStream_t own_stream = nullptr;
+    xrs::Pool* pool = nullptr;
+    // pinned host scratch for returning scalars / statuses
+    void* host_scratch = nullptr;
+    // device scratch for reductions / statuses (64 KiB)
+    void* dev_scratch = nullptr;
+    // profiler
+    uint32_t prof_mask = 0;
+    std::vector<xrs::ProfRecord> prof;
+    std::vector<hipEvent_t> event_cache;
+};
+
+namespace xrs {
+
+// RAII device buffer from the handle's pool.
+struct DevBuf {
+    xrs_handle_t h = nullptr;
+    void* p = nullptr;
+    size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(xrs_handle_t h_, size_t bytes_) : h(h_), bytes(bytes_) { p = bytes_ ? h_->pool->alloc(bytes_) : nullptr; }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : h(o.h), p(o.p), bytes(o.bytes) { o.p = nullptr; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        reset();
+        h = o.h; p = o.p; bytes = o.bytes; o.p = nullptr;
+        return *this;
+    }
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) h->pool->release(p);
+        p = nullptr;
+    }
+    double* d() const { return static_cast<double*>(p); }
+    template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Kernel-duration instrumentation (xrs_prof_begin/end).
+class KernelTimer {
+   public:
+    KernelTimer(xrs_handle_t h, uint32_t family, double flops, double bytes);
+    ~KernelTimer();
+
+   private:
+    xrs_handle_t h_;
+    bool on_;
+    ProfRecord rec_{};
+};
+
+void check_launch(const char* what);
+
+}  // namespace xrs
