@@ -1,0 +1,95 @@
+"""GPU parity of QC/CQ/QR/RQ/SVD (through the C-ABI) against the LAPACK-call oracle.
+
+Factors are not unique (pivot order, signs), so parity is judged on invariants, as the reference's own
+tests do (fullTensor_factorisations.cxx:26-276): reconstruction, orthogonality, singular values, and
+the exact rank of the reference's rank rule (blasLapackWrapper.cpp:268-272).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-12
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300)
+
+
+SHAPES = [(8, 5), (5, 8), (6, 6), (1, 4), (4, 1), (400, 128), (5120, 256), (2560, 128), (2560, 20), (20, 256),
+          (128, 2560), (256, 5120), (700, 300), (3, 3000)]
+
+
+@pytest.mark.parametrize("m,n", SHAPES)
+def test_qc_random(handle, ref, m, n):
+    A = np.random.default_rng(m * 31 + n).standard_normal((m, n))
+    Q, Cm, r = handle.qc(handle.array(A))
+    Qh, Ch = Q.numpy(), Cm.numpy()
+    _, _, rr = ref.qc(A)
+    assert r == rr == min(m, n)
+    assert _rel(Qh @ Ch, A) <= TOL
+    assert np.linalg.norm(Qh.T @ Qh - np.eye(r)) <= TOL * max(1, r)
+
+
+@pytest.mark.parametrize("m,n", SHAPES)
+def test_cq_random(handle, ref, m, n):
+    A = np.random.default_rng(m * 17 + n).standard_normal((m, n))
+    Cm, Q, r = handle.cq(handle.array(A))
+    Ch, Qh = Cm.numpy(), Q.numpy()
+    _, _, rr = ref.cq(A)
+    assert r == rr == min(m, n)
+    assert _rel(Ch @ Qh, A) <= TOL
+    assert np.linalg.norm(Qh @ Qh.T - np.eye(r)) <= TOL * max(1, r)
+
+
+@pytest.mark.parametrize("m,n,k", [(600, 200, 50), (300, 120, 1), (40, 30, 7), (2000, 256, 128), (256, 2000, 100)])
+@pytest.mark.parametrize("sign", [1.0, -1.0])
+def test_qc_cq_rank_deficient_matches_reference_rule(handle, ref, m, n, k, sign):
+    rng = np.random.default_rng(m + n + k)
+    A = sign * (rng.standard_normal((m, k)) @ rng.standard_normal((k, n)))
+    Q, Cm, r = handle.qc(handle.array(A))
+    _, _, rr = ref.qc(A)
+    assert r == rr
+    assert _rel(Q.numpy() @ Cm.numpy(), A) <= 1e-11
+    Cc, Qc, r2 = handle.cq(handle.array(A))
+    _, _, rr2 = ref.cq(A)
+    assert r2 == rr2
+    assert _rel(Cc.numpy() @ Qc.numpy(), A) <= 1e-11
+
+
+@pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (400, 128), (5120, 256), (128, 2560), (33, 700)])
+def test_qr_rq(handle, m, n):
+    A = np.random.default_rng(m + 3 * n).standard_normal((m, n))
+    k = min(m, n)
+    Q, R = handle.qr(handle.array(A))
+    Qh, Rh = Q.numpy(), R.numpy()
+    assert _rel(Qh @ Rh, A) <= TOL
+    assert np.linalg.norm(Qh.T @ Qh - np.eye(k)) <= TOL * k
+    R2, Q2 = handle.rq(handle.array(A))
+    R2h, Q2h = R2.numpy(), Q2.numpy()
+    assert _rel(R2h @ Q2h, A) <= TOL
+    assert np.linalg.norm(Q2h @ Q2h.T - np.eye(k)) <= TOL * k
+
+
+@pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (64, 64), (128, 128), (30, 200), (200, 30), (1, 5), (5, 1)])
+def test_svd(handle, ref, m, n):
+    A = np.random.default_rng(m * 5 + n).standard_normal((m, n))
+    U, S, Vt = handle.svd(handle.array(A))
+    Uh, Sh, Vh = U.numpy(), S.numpy(), Vt.numpy()
+    _, Sr, _ = ref.svd(A)
+    k = min(m, n)
+    assert np.all(np.diff(Sh) <= 0)
+    assert np.max(np.abs(Sh - Sr)) <= 1e-12 * Sr[0]
+    assert _rel((Uh * Sh[None, :]) @ Vh, A) <= TOL
+    assert np.linalg.norm(Uh.T @ Uh - np.eye(k)) <= TOL * k
+    assert np.linalg.norm(Vh @ Vh.T - np.eye(k)) <= TOL * k
+
+
+def test_svd_rank_deficient(handle, ref):
+    rng = np.random.default_rng(9)
+    A = rng.standard_normal((40, 6)) @ rng.standard_normal((6, 50))
+    U, S, Vt = handle.svd(handle.array(A))
+    Sh = S.numpy()
+    _, Sr, _ = ref.svd(A)
+    assert ref.svd_rank(Sh, 0, ref.EPSILON) == ref.svd_rank(Sr, 0, ref.EPSILON) == 6
+    assert np.max(np.abs(Sh - Sr)) <= 1e-12 * Sr[0]

@@ -1,0 +1,139 @@
+"""GPU parity of the TT hot path (move_core, round, <x,y>, frob_norm) against the oracle.
+
+Tolerances (BASELINE.md §3 / SURVEY §8(d)): inner products |d_gpu - d_ref| <= 1e-6 ||x|| ||y||;
+non-truncating round: identical ranks and ||T(gpu) - T(ref)|| <= 1e-6 ||T(x)||; truncating round:
+identical ranks and truncation errors equal to 1e-6 ||x||. The path is fp64 throughout, so the tests
+also assert the much tighter rounding-level bounds the implementation actually reaches.
+"""
+import numpy as np
+import pytest
+
+from xerus_amd import capi
+
+pytestmark = pytest.mark.gpu
+
+
+def _tt_diff_norm(ref, a_cores, b_cores):
+    """(||A - B||, ||B||) for two TTs without cancellation: the difference TT (block-diagonal sum
+    with -B) is orthogonalised by the oracle (move_core(0), backward stable) and its norm read off the
+    core, so the result is accurate to ~u*||B|| instead of the sqrt(u) floor of <A,A>-2<A,B>+<B,B>."""
+    A = ref.TT([c.copy() for c in a_cores])
+    B = ref.TT([c.copy() for c in b_cores])
+    nb = [c.copy() for c in B.cores]
+    nb[0] = -nb[0]
+    D = ref.tt_add(A, ref.TT(nb))
+    D.move_core(0)
+    B.move_core(0)
+    return D.frob_norm(), B.frob_norm()
+
+
+@pytest.mark.parametrize("dims,ranks", [
+    ([4, 5, 3, 4, 2], [3, 6, 5, 2]),
+    ([20] * 6, [16] * 5),
+    ([20] * 10, [128] * 9),   # cfg3 shape
+    ([20] * 12, [256] * 11),  # cfg4 shape
+])
+def test_dot(handle, ref, dims, ranks):
+    rng = ref.Rng(3)
+    x = ref.TT.random_raw(dims, ranks, rng)
+    y = ref.TT.random_raw(dims, ranks, rng)
+    gx = capi.TTDevice.from_cores(handle, x.cores)
+    gy = capi.TTDevice.from_cores(handle, y.cores)
+    d_ref = ref.dot(x, y)
+    d_gpu = gx.dot(gy)
+    nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
+    assert abs(d_gpu - d_ref) <= 1e-12 * nx * ny
+    assert abs(gx.dot(gx) - nx * nx) <= 1e-12 * nx * nx
+
+
+@pytest.mark.parametrize("dims,ranks", [([4, 5, 3, 4, 2], [3, 6, 5, 2]), ([3, 3, 3, 3], [9, 9, 9]),
+                                        ([20] * 6, [40] * 5), ([20] * 8, [128] * 7)])
+def test_random_move_core_left(handle, ref, dims, ranks):
+    """TTTensor::random = raw N(0,1) cores + move_core(0) (ttNetwork.h:129-157)."""
+    rng = ref.Rng()
+    x = ref.TT.random_raw(dims, ranks, rng)
+    g = capi.TTDevice.from_cores(handle, x.cores)
+    y = x.copy()
+    y.move_core(0)
+    g.move_core(0)
+    assert g.ranks == y.ranks
+    gc = g.cores()
+    for c in gc[1:]:
+        M = c.reshape(c.shape[0], -1)
+        assert np.linalg.norm(M @ M.T - np.eye(M.shape[0])) <= 1e-12 * M.shape[0]
+    diff, nrm = _tt_diff_norm(ref, gc, y.cores)
+    assert diff <= 1e-12 * nrm
+
+
+def test_move_core_right_and_back(handle, ref):
+    rng = ref.Rng(5)
+    x = ref.TT.random([6, 5, 4, 7, 3], [4, 8, 8, 3], rng)
+    g = capi.TTDevice.from_cores(handle, x.cores, canonicalized=True, core_position=0)
+    g.move_core(3)
+    y = x.copy()
+    y.move_core(3)
+    assert g.ranks == y.ranks
+    gc = g.cores()
+    for c in gc[:3]:
+        M = c.reshape(-1, c.shape[2])
+        assert np.linalg.norm(M.T @ M - np.eye(M.shape[1])) <= 1e-12 * M.shape[1]
+    diff, nrm = _tt_diff_norm(ref, gc, y.cores)
+    assert diff <= 1e-12 * nrm
+    assert abs(g.frob_norm() - y.frob_norm()) <= 1e-12 * nrm
+
+
+@pytest.mark.parametrize("dims,ranks", [([4, 5, 3, 4, 2], [3, 6, 5, 2]), ([20] * 6, [40] * 5),
+                                        ([20] * 10, [128] * 9)])
+def test_round_non_truncating(handle, ref, dims, ranks):
+    rng = ref.Rng(11)
+    x = ref.TT.random(dims, ranks, rng)
+    g = capi.TTDevice.from_cores(handle, x.cores, canonicalized=True, core_position=0)
+    y = x.copy()
+    y.round(max(ranks))
+    g.round(max(ranks))
+    assert g.ranks == y.ranks == x.ranks
+    gc = g.cores()
+    diff, nrm = _tt_diff_norm(ref, gc, x.cores)
+    assert diff <= 1e-10 * nrm          # bar: 1e-6
+    for c in gc[1:]:
+        M = c.reshape(c.shape[0], -1)
+        assert np.linalg.norm(M @ M.T - np.eye(M.shape[0])) <= 1e-12 * M.shape[0]
+
+
+@pytest.mark.parametrize("dims,ranks,target", [([4, 5, 3, 4, 2], [3, 6, 5, 2], 2), ([6] * 5, [20] * 4, 7),
+                                               ([20] * 6, [40] * 5, 17), ([20] * 10, [128] * 9, 64)])
+def test_round_truncating(handle, ref, dims, ranks, target):
+    rng = ref.Rng(13)
+    x = ref.TT.random(dims, ranks, rng)
+    g = capi.TTDevice.from_cores(handle, x.cores, canonicalized=True, core_position=0)
+    y = x.copy()
+    y.round(target)
+    g.round(target)
+    assert g.ranks == y.ranks
+    e_ref, nrm = _tt_diff_norm(ref, y.cores, x.cores)
+    e_gpu, _ = _tt_diff_norm(ref, g.cores(), x.cores)
+    assert abs(e_gpu - e_ref) <= 1e-6 * nrm
+
+
+def test_round_sum_recovers_ranks(handle, ref):
+    """x + x has doubled ranks; round() must cut them back (SVD eps rule, tensor.cpp:1469-1474)."""
+    rng = ref.Rng(17)
+    x = ref.TT.random([5, 4, 6, 3, 5], [4, 7, 6, 3], rng)
+    s = ref.tt_add(x, x)
+    g = capi.TTDevice.from_cores(handle, s.cores)
+    y = s.copy()
+    y.round(100)
+    g.round(100)
+    assert g.ranks == y.ranks == x.ranks
+    diff, nrm = _tt_diff_norm(ref, g.cores(), [2 * c if i == 0 else c for i, c in enumerate(x.cores)])
+    assert diff <= 1e-10 * nrm
+
+
+def test_tt_errors(handle, ref):
+    rng = ref.Rng(1)
+    x = ref.TT.random([3, 3, 3], [2, 2], rng)
+    g = capi.TTDevice.from_cores(handle, x.cores, canonicalized=True, core_position=0)
+    with pytest.raises(capi.XrsError):
+        g.round([0, 2])
+    with pytest.raises(capi.XrsError):
+        g.move_core(5)

@@ -253,9 +253,14 @@ class DeviceArray:
     def __init__(self, handle: Handle, shape: tuple, ptr: int | None = None, owned: bool = True):
         self.handle = handle
         self.shape = tuple(shape)
-        self.size = int(np.prod(self.shape)) if self.shape else 1
+        self.capacity = self.size
         self.owned = owned and ptr is None
-        self.ptr = ptr if ptr is not None else (handle.malloc(max(8, self.size * 8)))
+        self.ptr = ptr if ptr is not None else (handle.malloc(max(8, self.capacity * 8)))
+
+    @property
+    def size(self) -> int:
+        """Elements of the current shape (a factorisation may shrink the shape to the rank)."""
+        return int(np.prod(self.shape)) if self.shape else 1
 
     @classmethod
     def from_host(cls, handle: Handle, a: np.ndarray) -> "DeviceArray":
@@ -267,6 +272,7 @@ class DeviceArray:
 
     def numpy(self) -> np.ndarray:
         out = np.empty(self.shape, dtype=np.float64)
+        assert self.size <= self.capacity, "shape exceeds the allocation"
         if self.size:
             _check("xrs_download", self.handle.lib.xrs_download(self.handle.h, out.ctypes.data_as(_DP), _DP(self.ptr),
                                                                self.size))
@@ -276,6 +282,109 @@ class DeviceArray:
         if self.owned and self.ptr:
             self.handle.free(self.ptr)
         self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class TTDevice:
+    """A TT tensor whose cores live in the handle's device pool (core k: (r[k], n[k], r[k+1]) row-major).
+
+    Thin wrapper over xrs_tt_* — the TT hot path runs entirely on the GPU."""
+
+    def __init__(self, handle: Handle, dims, ranks, ptrs, canonicalized=False, core_position=0):
+        self.handle = handle
+        self.dims = [int(x) for x in dims]
+        self.r = [int(x) for x in ranks]        # d+1 entries
+        self.ptrs = list(ptrs)
+        self.canonicalized = canonicalized
+        self.core_position = core_position
+
+    @classmethod
+    def from_cores(cls, handle: Handle, cores, canonicalized=False, core_position=0) -> "TTDevice":
+        dims = [c.shape[1] for c in cores]
+        ranks = [cores[0].shape[0]] + [c.shape[2] for c in cores]
+        ptrs = []
+        for c in cores:
+            c = np.ascontiguousarray(c, dtype=np.float64)
+            p = handle.malloc(max(8, c.size * 8))
+            _check("xrs_upload", handle.lib.xrs_upload(handle.h, _DP(p), c.ctypes.data_as(_DP), c.size))
+            ptrs.append(p)
+        return cls(handle, dims, ranks, ptrs, canonicalized, core_position)
+
+    @property
+    def order(self):
+        return len(self.dims)
+
+    @property
+    def ranks(self):
+        return self.r[1:-1]
+
+    def cores(self):
+        out = []
+        for k, p in enumerate(self.ptrs):
+            shp = (self.r[k], self.dims[k], self.r[k + 1])
+            a = np.empty(shp)
+            _check("xrs_download", self.handle.lib.xrs_download(self.handle.h, a.ctypes.data_as(_DP), _DP(p), a.size))
+            out.append(a)
+        return out
+
+    def _arrays(self):
+        d = self.order
+        n = _arr(self.dims)
+        r = _arr(self.r)
+        cores = (_DP * d)(*[_DP(p) for p in self.ptrs])
+        return n, r, cores
+
+    def _writeback(self, r, cores):
+        self.r = [int(r[i]) for i in range(self.order + 1)]
+        self.ptrs = [int(cores[i] or 0) for i in range(self.order)]
+
+    def move_core(self, position: int, keep_rank: bool = False):
+        n, r, cores = self._arrays()
+        st = self.handle.lib.xrs_tt_move_core(self.handle.h, self.order, n, r, cores, int(self.canonicalized),
+                                              self.core_position, position, int(keep_rank))
+        self._writeback(r, cores)
+        _check("xrs_tt_move_core", st)
+        self.canonicalized, self.core_position = True, position
+
+    def round(self, max_ranks, eps: float = 8 * np.finfo(float).eps):
+        d = self.order
+        if isinstance(max_ranks, (int, np.integer)):
+            max_ranks = [int(max_ranks)] * (d - 1)
+        n, r, cores = self._arrays()
+        mr = _arr(list(max_ranks) + [1])
+        st = self.handle.lib.xrs_tt_round(self.handle.h, d, n, r, cores, int(self.canonicalized), self.core_position,
+                                          mr, eps)
+        self._writeback(r, cores)
+        _check("xrs_tt_round", st)
+        self.canonicalized, self.core_position = True, 0
+
+    def dot(self, other: "TTDevice") -> float:
+        out = C.c_double()
+        d = self.order
+        n = _arr(self.dims)
+        xc = (_DP * d)(*[_DP(p) for p in self.ptrs])
+        yc = (_DP * d)(*[_DP(p) for p in other.ptrs])
+        _check("xrs_tt_dot", self.handle.lib.xrs_tt_dot(self.handle.h, C.byref(out), d, n, _arr(self.r), xc,
+                                                      _arr(other.r), yc))
+        return out.value
+
+    def frob_norm(self) -> float:
+        if self.canonicalized:
+            k = self.core_position
+            size = self.r[k] * self.dims[k] * self.r[k + 1]
+            return self.handle.nrm2(DeviceArray(self.handle, (size,), ptr=self.ptrs[k], owned=False))
+        return float(np.sqrt(max(0.0, self.dot(self))))
+
+    def free(self):
+        for p in self.ptrs:
+            if p:
+                self.handle.free(p)
+        self.ptrs = [0] * len(self.ptrs)
 
     def __del__(self):
         try:

@@ -169,6 +169,8 @@ static void launch_tiles(xrs_handle_t h, const double* A, size_t lda, bool ta, c
                          double* C, int M, int N, int K, int splits, int kps, double alpha, double* slab) {
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     dim3 grid(unsigned(tiles_m * tiles_n), 1, unsigned(splits));
+    KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(M) * double(N) * double(K),
+                      8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GEMM_LAUNCH(TA_, TB_)                                                                             \
     hipLaunchKernelGGL((k_gemm_f64<BM, BN, TA_, TB_>), grid, dim3(256), 0, h->stream, A, lda, B, ldb, C, M, N, K, \
                        kps, alpha, slab, tiles_m)
@@ -185,9 +187,6 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
     if (Ms == 0 || Ns == 0) return;
     XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
     const int M = int(Ms), N = int(Ns), K = int(Ks);
-    const double flops = 2.0 * double(M) * double(N) * double(K);
-    const double bytes = 8.0 * (double(M) * K + double(K) * N + double(M) * N);
-    KernelTimer timer(h, XRS_KFAM_GEMM, flops, bytes);
     if (K == 0) {
         XRS_HIP(hipMemsetAsync(C, 0, size_t(M) * N * 8, h->stream));
         return;
@@ -216,6 +215,7 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
     if (splits > 1) {
         const size_t MN = size_t(M) * N;
         const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
+        KernelTimer timer(h, XRS_KFAM_ELEMWISE, double(MN) * splits, 8.0 * double(MN) * (splits + 1));
         hipLaunchKernelGGL(k_splitk_reduce, dim3(blocks), dim3(256), 0, h->stream, C, slab.d(), MN, splits, alpha);
         check_launch("k_splitk_reduce");
     }

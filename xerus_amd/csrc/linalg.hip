@@ -1,0 +1,328 @@
+// Factorisation drivers with the reference's semantics (blasLapackWrapper.cpp:201-498) on top of the
+// GEMM / Cholesky / TRSM / QRCP / Jacobi kernels, plus their C-ABI entry points.
+//
+// Orthogonalisation (the hot path of TT rounding) is CholeskyQR2 on fp64 MFMA GEMMs:
+//   G = A^T A, L1 = chol(G - tau I), Q1 = A L1^{-T}, G2 = Q1^T Q1, L2 = chol(G2), Q = Q1 L2^{-T}, R = (L1 L2)^T.
+// The first Cholesky is shifted DOWN by tau = 4 (m + 2n) u ||A||_F^2: if it succeeds, the rounding errors
+// of forming G and of the factorisation are covered and sigma_min(A) >= sqrt(tau/2) is *proven*
+// (certified). A certified A has full numerical rank for the reference's QC rule (|R_kk| >= 16 u R_00) and
+// no singular value below eps*sigma_0 for eps < sqrt(tau/2)/||A||_F, so rank decisions need no pivoting
+// and no SVD. If certification fails, shifted CholeskyQR3 (Fukaya et al., SIAM J. Sci. Comput. 2020)
+// still yields an orthonormal Q for any A with kappa < 1/u; exact rank semantics then come from the
+// single-workgroup dgeqp3 emulation applied to the small n x n triangular factor, with the sign of
+// dgeqp3's R_00 taken from A itself (it is -sign(A[0][p]) for the first max-norm column p).
+#include <cmath>
+
+#include "smallla.hpp"
+
+namespace xrs {
+
+constexpr double kU = 1.1102230246251565e-16;       // unit roundoff 2^-53
+constexpr double kDblEps = 2.220446049250313e-16;   // std::numeric_limits<double>::epsilon()
+
+void transpose(xrs_handle_t h, double* out, const double* in, size_t rows, size_t cols) {
+    const size_t dims[2] = {rows, cols};
+    const size_t shuf[2] = {1, 0};
+    permute(h, out, in, 2, dims, shuf);
+}
+
+int read_status(xrs_handle_t h, const int* status_dev, int count, int* host_out) {
+    int* hs = static_cast<int*>(h->host_scratch);
+    XRS_HIP(hipMemcpyAsync(hs, status_dev, size_t(count) * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    int any = 0;
+    for (int i = 0; i < count; ++i) {
+        host_out[i] = hs[i];
+        any |= hs[i];
+    }
+    return any;
+}
+
+// first index of the max-norm column (rows=false) or row (rows=true) and the entry A[0][p] / A[p][0]
+__global__ void __launch_bounds__(1024) k_argmax_norm(const double* __restrict__ A, int m, int n, int rows,
+                                                      double* __restrict__ out) {
+    __shared__ double sv[16];
+    __shared__ int si[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int cnt = rows ? m : n, len = rows ? n : m;
+    double best = -1.0;
+    int bi = cnt;
+    for (int j = wave; j < cnt; j += 16) {
+        double s = 0.0;
+        for (int i = lane; i < len; i += 64) {
+            const double v = rows ? A[size_t(j) * n + i] : A[size_t(i) * n + j];
+            s += v * v;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+        if (s > best) { best = s; bi = j; }
+    }
+    if (lane == 0) { sv[wave] = best; si[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+        double bv = -1.0;
+        int b = cnt;
+        for (int w = 0; w < 16; ++w)
+            if (sv[w] > bv || (sv[w] == bv && si[w] < b)) { bv = sv[w]; b = si[w]; }
+        out[0] = double(b);
+        out[1] = rows ? A[size_t(b) * n] : A[b];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_dev_identity(const double* __restrict__ G, int n, double* __restrict__ out) {
+    __shared__ double red[4];
+    double mx = 0.0;
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+        const double d = fabs(G[e] - ((e / n) == (e % n) ? 1.0 : 0.0));
+        mx = (d > mx || d != d) ? d : mx;   // NaN propagates
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double t = __shfl_xor(mx, o, 64);
+        mx = (t > mx || t != t) ? t : mx;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = red[0];
+        for (int i = 1; i < 4; ++i) m = (red[i] > m || red[i] != red[i]) ? red[i] : m;
+        out[0] = m;
+    }
+}
+
+static double max_abs_dev_identity(xrs_handle_t h, const double* G, size_t n) {
+    double* out = static_cast<double*>(h->dev_scratch) + 32;
+    hipLaunchKernelGGL(k_dev_identity, dim3(1), dim3(256), 0, h->stream, G, int(n), out);
+    check_launch("k_dev_identity");
+    double* hs = static_cast<double*>(h->host_scratch) + 32;
+    XRS_HIP(hipMemcpyAsync(hs, out, 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    const double v = hs[0];
+    return (v == v) ? v : 1e300;
+}
+
+// dgeqp3's R_00 > 0 iff the first entry of the pivot column is negative (dlarfg: beta = -sign(alpha)*norm);
+// for a single-row problem (dlarfg with N = 1) R_00 = alpha itself.
+static bool reference_r00_positive(xrs_handle_t h, const double* A, size_t m, size_t n, bool rows) {
+    double* out = static_cast<double*>(h->dev_scratch) + 16;
+    hipLaunchKernelGGL(k_argmax_norm, dim3(1), dim3(1024), 0, h->stream, A, int(m), int(n), int(rows), out);
+    check_launch("k_argmax_norm");
+    double* hs = static_cast<double*>(h->host_scratch) + 16;
+    XRS_HIP(hipMemcpyAsync(hs, out, 16, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    const double alpha = hs[1];
+    const size_t len = rows ? n : m;
+    if (len <= 1) return alpha > 0.0;
+    return alpha < 0.0 || (alpha == 0.0 && std::signbit(alpha));
+}
+
+// ------------------------------------------------------------------------------------------------
+// CholeskyQR2 / shifted CholeskyQR3. Tall: A (m x n) = Q R. Wide: A (m x n) = L Q.
+OrthResult orthogonalize(xrs_handle_t h, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL) {
+    const size_t N = wide ? m : n;   // Gram size
+    const size_t M = wide ? n : m;   // long dimension
+    XRS_REQUIRE(N >= 1 && M >= N, "orthogonalize: need a tall (or, wide=true, a wide) matrix");
+    OrthResult res{false, 0.0, false};
+    if (N > size_t(kSmallMax)) throw Error{XRS_EINVAL, "orthogonalize: rank > 512 not supported yet"};
+    const int Ni = int(N), nvec = int(M);
+    DevBuf G(h, N * N * 8), Dv(h, N * 32 * 8), L1(h, N * N * 8), Q1(h, m * n * 8), st(h, 64);
+    auto gram = [&](double* out, const double* X) {
+        if (wide) gemm(h, out, N, N, 1.0, X, n, false, M, X, n, true);   // X X^T
+        else gemm(h, out, N, N, 1.0, X, n, true, M, X, n, false);        // X^T X
+    };
+    auto solve = [&](const double* L, const double* Y, double* X) {
+        trsm(h, wide, L, Dv.d(), Ni, Y, n, X, n, nvec);
+    };
+    // ---- CholeskyQR2 with a certifying downward shift on the first factorisation
+    const double tau_rel = 4.0 * double(M + 2 * N) * kU;
+    int* stv = st.as<int>();
+    gram(G.d(), A);
+    potrf(h, G.d(), Ni, -tau_rel, Dv.d(), stv + 0);
+    solve(G.d(), A, Q1.d());
+    gram(L1.d(), Q1.d());
+    potrf(h, L1.d(), Ni, 0.0, Dv.d(), stv + 1);
+    solve(L1.d(), Q1.d(), Q);
+    if (wide) gemm(h, RL, N, N, 1.0, G.d(), N, false, N, L1.d(), N, false);   // L = L1 L2
+    else gemm(h, RL, N, N, 1.0, L1.d(), N, true, N, G.d(), N, true);          // R = L2^T L1^T
+    int sts[3] = {0, 0, 0};
+    if (read_status(h, stv, 2, sts) == 0) {
+        res.certified = true;
+        res.cert_ratio = std::sqrt(0.5 * tau_rel);
+        return res;
+    }
+    // ---- shifted CholeskyQR3: valid for any kappa(A) < 1/u
+    res.robust = true;
+    const double s_rel = 11.0 * (double(M) * N + double(N) * (N + 1)) * kU;
+    DevBuf Q2(h, m * n * 8), L2(h, N * N * 8), T(h, N * N * 8);
+    gram(G.d(), A);
+    potrf(h, G.d(), Ni, s_rel, Dv.d(), stv + 0);
+    solve(G.d(), A, Q1.d());
+    gram(L1.d(), Q1.d());
+    potrf(h, L1.d(), Ni, 0.0, Dv.d(), stv + 1);
+    solve(L1.d(), Q1.d(), Q2.d());
+    gram(L2.d(), Q2.d());
+    potrf(h, L2.d(), Ni, 0.0, Dv.d(), stv + 2);
+    solve(L2.d(), Q2.d(), Q);
+    if (wide) {  // L = L1 L2 L3
+        gemm(h, T.d(), N, N, 1.0, G.d(), N, false, N, L1.d(), N, false);
+        gemm(h, RL, N, N, 1.0, T.d(), N, false, N, L2.d(), N, false);
+    } else {     // R = L3^T L2^T L1^T
+        gemm(h, T.d(), N, N, 1.0, L2.d(), N, true, N, L1.d(), N, true);
+        gemm(h, RL, N, N, 1.0, T.d(), N, false, N, G.d(), N, true);
+    }
+    if (read_status(h, stv, 3, sts) == 0) {
+        // Cholesky-based passes can "succeed" on an exactly singular Gram with meaningless factors:
+        // accept only a verified orthonormal Q (||Q^T Q - I||_max <= 64 n u), else fall through.
+        gram(T.d(), Q);
+        if (max_abs_dev_identity(h, T.d(), N) <= 64.0 * double(N) * kU) return res;
+    }
+    // ---- last resort: unpivoted Householder (exact dgeqrf + dorgqr emulation, one workgroup)
+    if (!wide) {
+        qrcp(h, A, m, n, Q, RL, false, false, false);
+    } else {
+        DevBuf At(h, m * n * 8), Qt(h, m * n * 8), Rt(h, m * m * 8);
+        transpose(h, At.d(), A, m, n);                     // n x m
+        qrcp(h, At.d(), n, m, Qt.d(), Rt.d(), false, false, false);   // A^T = Qt Rt
+        transpose(h, Q, Qt.d(), n, m);                     // Q = Qt^T (m x n)
+        transpose(h, RL, Rt.d(), m, m);                    // L = Rt^T
+    }
+    return res;
+}
+
+// ------------------------------------------------------------------------------------------------
+// QC with the reference's rank rule (blasLapackWrapper.cpp:243-305).
+static bool small_problem(size_t m, size_t n) { return m * n <= 4096 || std::min(m, n) <= 8; }
+
+static void compact_cols(xrs_handle_t h, double* dst, size_t ldd, const double* src, size_t lds, size_t rows, size_t cols) {
+    if (ldd == lds && dst == src) return;
+    XRS_HIP(hipMemcpy2DAsync(dst, ldd * 8, src, lds * 8, cols * 8, rows, hipMemcpyDeviceToDevice, h->stream));
+}
+
+size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C) {
+    XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
+    const size_t k = std::min(m, n);
+    if (m < n || n > size_t(kSmallMax) || small_problem(m, n)) {
+        DevBuf Qf(h, m * k * 8);
+        const size_t r = qrcp(h, A, m, n, Qf.d(), C, true, false, true);
+        compact_cols(h, Q, r, Qf.d(), k, m, r);
+        return r;
+    }
+    OrthResult o = orthogonalize(h, A, m, n, false, Q, C);
+    // certified: sigma_min >= cert*||A||_F > 16 u R_00 (R_00 <= ||A||_F) -> rank n
+    if (o.certified && o.cert_ratio > 64.0 * kDblEps) return n;
+    if (!reference_r00_positive(h, A, m, n, false)) return n;  // reference never reduces rank then
+    // exact pivoted rank on the triangular factor (same column norms as A up to rounding)
+    DevBuf Rc(h, n * n * 8), Q2(h, n * n * 8), Cq(h, n * n * 8), Qo(h, m * n * 8);
+    XRS_HIP(hipMemcpyAsync(Rc.d(), C, n * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    const size_t r = qrcp(h, Rc.d(), n, n, Q2.d(), Cq.d(), true, true, true);
+    XRS_HIP(hipMemcpyAsync(Qo.d(), Q, m * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    gemm(h, Q, m, r, 1.0, Qo.d(), n, false, n, Q2.d(), n, false);   // Q = Q * Q2[:, :r]  (ldb = n, first r cols)
+    XRS_HIP(hipMemcpyAsync(C, Cq.d(), r * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    return r;
+}
+
+// CQ: the reference runs col-major dgeqp3 on A^T (blasLapackWrapper.cpp:317-371), i.e. QC of A^T.
+size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double* Q) {
+    XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
+    const size_t k = std::min(m, n);
+    if (n < m || m > size_t(kSmallMax) || small_problem(m, n)) {
+        DevBuf At(h, m * n * 8), Qt(h, n * k * 8), Ct(h, k * m * 8);
+        transpose(h, At.d(), A, m, n);                           // n x m
+        const size_t r = qrcp(h, At.d(), n, m, Qt.d(), Ct.d(), true, false, true);   // A^T = Qt Ct
+        DevBuf Qc(h, n * r * 8 + 8);
+        compact_cols(h, Qc.d(), r, Qt.d(), k, n, r);
+        transpose(h, Q, Qc.d(), n, r);                            // Q = Qt^T  (r x n)
+        transpose(h, C, Ct.d(), r, m);                            // C = Ct^T  (m x r)
+        return r;
+    }
+    OrthResult o = orthogonalize(h, A, m, n, true, Q, C);        // A = L Q, C := L (m x m)
+    if (o.certified && o.cert_ratio > 64.0 * kDblEps) return m;
+    if (!reference_r00_positive(h, A, m, n, true)) return m;
+    DevBuf Lt(h, m * m * 8), Q2(h, m * m * 8), C2(h, m * m * 8), Qo(h, m * n * 8);
+    transpose(h, Lt.d(), C, m, m);                                // A^T = Q^T L^T
+    const size_t r = qrcp(h, Lt.d(), m, m, Q2.d(), C2.d(), true, true, true);   // L^T P = Q2 R2
+    XRS_HIP(hipMemcpyAsync(Qo.d(), Q, m * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    gemm(h, Q, r, n, 1.0, Q2.d(), m, true, m, Qo.d(), n, false);   // Q = Q2[:, :r]^T Q
+    transpose(h, C, C2.d(), r, m);                                // C = C2^T (m x r)
+    return r;
+}
+
+void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* R) {
+    XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
+    if (m >= n && n <= size_t(kSmallMax) && !small_problem(m, n)) {
+        orthogonalize(h, A, m, n, false, Q, R);
+        return;
+    }
+    qrcp(h, A, m, n, Q, R, false, false, false);
+}
+
+void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* Q) {
+    XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
+    if (m <= n && m <= size_t(kSmallMax) && !small_problem(m, n)) {
+        orthogonalize(h, A, m, n, true, Q, R);
+        return;
+    }
+    const size_t k = std::min(m, n);
+    DevBuf At(h, m * n * 8), Qt(h, n * k * 8), Rt(h, k * m * 8);
+    transpose(h, At.d(), A, m, n);
+    qrcp(h, At.d(), n, m, Qt.d(), Rt.d(), false, false, false);   // A^T = Qt Rt
+    transpose(h, Q, Qt.d(), n, k);
+    transpose(h, R, Rt.d(), k, m);
+}
+
+void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
+    XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
+    XRS_REQUIRE(std::min(m, n) <= size_t(kSmallMax), "svd: min(m, n) > 512 not supported yet");
+    if (m <= n) {
+        jacobi_svd_rows(h, A, int(m), int(n), U, S, Vt);
+        return;
+    }
+    DevBuf At(h, m * n * 8), Ut(h, n * n * 8), Vtt(h, n * m * 8);
+    transpose(h, At.d(), A, m, n);                                  // n x m
+    jacobi_svd_rows(h, At.d(), int(n), int(m), Ut.d(), S, Vtt.d());  // A^T = Ut S Vtt
+    transpose(h, U, Vtt.d(), n, m);                                  // U = Vtt^T (m x n)
+    transpose(h, Vt, Ut.d(), n, n);                                  // Vt = Ut^T
+}
+
+}  // namespace xrs
+
+using namespace xrs;
+
+extern "C" {
+
+int xrs_qc(xrs_handle_t h, double* Q, double* C, size_t* rank, const double* A, size_t m, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && Q && C && rank && A, "null argument");
+        *rank = qc(h, A, m, n, Q, C);
+    });
+}
+
+int xrs_cq(xrs_handle_t h, double* C, double* Q, size_t* rank, const double* A, size_t m, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && Q && C && rank && A, "null argument");
+        *rank = cq(h, A, m, n, C, Q);
+    });
+}
+
+int xrs_qr(xrs_handle_t h, double* Q, double* R, const double* A, size_t m, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && Q && R && A, "null argument");
+        qr(h, A, m, n, Q, R);
+    });
+}
+
+int xrs_rq(xrs_handle_t h, double* R, double* Q, const double* A, size_t m, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && Q && R && A, "null argument");
+        rq(h, A, m, n, R, Q);
+    });
+}
+
+int xrs_svd(xrs_handle_t h, double* U, double* S, double* Vt, const double* A, size_t m, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && U && S && Vt && A, "null argument");
+        svd(h, A, m, n, U, S, Vt);
+    });
+}
+
+}  // extern "C"

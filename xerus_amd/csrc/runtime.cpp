@@ -1,6 +1,8 @@
 // Handle, stream, caching allocator, profiler and the runtime part of the C-ABI.
 #include "runtime.hpp"
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 namespace xrs {
@@ -89,9 +91,25 @@ KernelTimer::~KernelTimer() {
     h_->prof.push_back(rec_);
 }
 
+static int sync_debug() {
+    static int v = [] {
+        const char* e = std::getenv("XRS_SYNC_DEBUG");
+        return (e && *e && *e != '0') ? 1 : 0;
+    }();
+    return v;
+}
+
 void check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw Error{XRS_EHIP, std::string(what) + ": " + hipGetErrorString(e)};
+    if (sync_debug()) {
+        std::fprintf(stderr, "[xrs] launched %s\n", what);
+        std::fflush(stderr);
+        e = hipDeviceSynchronize();
+        std::fprintf(stderr, "[xrs]   done %s: %s\n", what, hipGetErrorString(e));
+        std::fflush(stderr);
+        if (e != hipSuccess) throw Error{XRS_EHIP, std::string(what) + ": " + hipGetErrorString(e)};
+    }
 }
 
 }  // namespace xrs

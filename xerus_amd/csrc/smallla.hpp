@@ -1,0 +1,45 @@
+// Launch wrappers of the small dense kernels (smallla.hip) and the factorisation drivers (linalg.cpp).
+#pragma once
+#include "elementwise.hpp"
+
+namespace xrs {
+
+constexpr int kSmallMax = 512;  // largest n handled by the single-workgroup kernels
+
+// G (n x n) := L with G + shift_rel*trace(G)*I = L L^T (lower, upper zeroed); Dinv: n x 32 inverses of the
+// diagonal blocks. *status_dev = 0 on success, else 1 + first failing column; info_dev[0] = trace(G)
+// (may be null). Enqueued only.
+void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int* status_dev, double* info_dev = nullptr);
+// X = L^{-1} Y. cols=false: the RHS vectors are the nvec rows of Y (ld ldy); cols=true: the nvec columns.
+void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n, const double* Y, size_t ldy, double* X,
+          size_t ldx, int nvec);
+// Exact dgeqp3/dgeqrf + dorgqr emulation on A (m x n row-major). pivot=false -> unpivoted Householder QR.
+// abs_r00: use |R_00| in the rank rule (when the caller already knows the reference's R_00 is positive).
+// Q: m x min(m,n) (ld min(m,n)), C: rank x n (C rows beyond rank untouched). Returns the rank (synchronises).
+size_t qrcp(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C, bool pivot, bool abs_r00,
+            bool rank_rule);
+// One-sided Jacobi SVD of the rows of W (p x q, p <= q): U (p x p), S (p), Vt (p x q), S descending.
+void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, double* S, double* Vt);
+
+struct OrthResult {
+    bool certified;   // sigma_min(A) >= cert_ratio * ||A||_F proven (Cholesky of the shifted Gram succeeded)
+    double cert_ratio;
+    bool robust;      // the shifted CholeskyQR3 / Householder path was needed
+};
+
+// Tall A (m x n, m >= n): A = Q R, Q m x n orthonormal columns, R n x n upper triangular.
+// Wide B (m x n, m <= n) with wide=true: B = L Q, L m x m lower, Q m x n orthonormal rows.
+OrthResult orthogonalize(xrs_handle_t h, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL);
+
+// Reference-semantics factorisations (blasLapackWrapper.cpp:235-498); device buffers as in xerus_amd.h.
+size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C);
+size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double* Q);
+void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* R);
+void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* Q);
+void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt);
+
+// helpers
+void transpose(xrs_handle_t h, double* out, const double* in, size_t rows, size_t cols);
+int read_status(xrs_handle_t h, const int* status_dev, int count, int* host_out);
+
+}  // namespace xrs

@@ -1,0 +1,298 @@
+// TT hot path on device: move_core (transfer_core sweeps), round (orthogonalise + truncate), <x,y>.
+//
+// Reference: TTNetwork::move_core (ttNetwork.cpp:582-628) -> TensorNetwork::transfer_core
+// (tensorNetwork.cpp:821-909); TTNetwork::round (ttNetwork.cpp:644-665) -> round_edge
+// (tensorNetwork.cpp:678-818); <x,y> = value_t(x(i&0)*y(i&0)).
+//
+// Cores live in HBM for the whole sweep; core k is (r[k], n[k], r[k+1]) row-major. Every matricisation
+// used here is a free reshape of that layout, so — unlike the reference, which reshuffles the zipper
+// intermediates (27 permutations per <x,y>) — no permutation kernel is needed on the TT path: the GEMM
+// transpose flags absorb them.
+//
+// round(): the left-to-right sweep orthogonalises with CholeskyQR2 (certified) instead of pivoted QR;
+// the right-to-left sweep factors each core B = L Q (wide CholeskyQR2) and takes the SVD of the small
+// r x r factor L, whose singular values are those of the unfolding (the reference computes them as the
+// SVD of C_f^T C_t^T, round_edge :745-779 — identical values because the left core is orthogonal).
+// When the factorisation is certified (sigma_min >= c ||B||_F, see linalg.hip), eps < c and
+// max_rank >= r, no singular value can be cut, so the SVD is skipped and B = L Q is used directly:
+// same represented tensor, same ranks, different (equally valid) orthogonal gauge.
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "smallla.hpp"
+
+namespace xrs {
+
+namespace {
+
+struct TT {
+    xrs_handle_t h;
+    size_t d;
+    const size_t* n;
+    size_t* r;      // d + 1 ranks, r[0] = r[d] = 1
+    double** core;
+
+    size_t rows_left(size_t k) const { return r[k] * n[k]; }      // (r_k n_k) x r_{k+1}
+    size_t cols_right(size_t k) const { return n[k] * r[k + 1]; }  // r_k x (n_k r_{k+1})
+    size_t size(size_t k) const { return r[k] * n[k] * r[k + 1]; }
+
+    double* alloc(size_t elems) { return static_cast<double*>(h->pool->alloc(std::max<size_t>(elems, 1) * 8)); }
+    void release(double* p) { if (p) h->pool->release(p); }
+    void replace(size_t k, double* p) { release(core[k]); core[k] = p; }
+};
+
+// reduce_to_maximal_ranks (ttNetwork.cpp:370-402)
+std::vector<size_t> maximal_ranks(const TT& t) {
+    std::vector<size_t> rk(t.r + 1, t.r + t.d);  // internal ranks r[1..d-1]
+    size_t cur = 1;
+    for (size_t i = 0; i + 1 < t.d; ++i) {
+        cur *= t.n[i];
+        if (cur < rk[i]) rk[i] = cur;
+        else cur = rk[i];
+    }
+    cur = 1;
+    for (size_t i = 1; i < t.d; ++i) {
+        cur *= t.n[t.d - i];
+        if (cur < rk[t.d - i - 1]) rk[t.d - i - 1] = cur;
+        else cur = rk[t.d - i - 1];
+    }
+    return rk;
+}
+
+bool exceeds_maximal_ranks(const TT& t) {
+    const auto mx = maximal_ranks(t);
+    for (size_t i = 0; i + 1 < t.d; ++i)
+        if (t.r[i + 1] != mx[i]) return true;
+    return false;
+}
+
+// transfer_core(k -> k+1): posA = last mode -> QC (or QR), posB = 0 -> R * next (tensorNetwork.cpp:842-848, 873)
+void transfer_right(TT& t, size_t k, bool rank_reduce) {
+    const size_t m = t.rows_left(k), nn = t.r[k + 1], kmax = std::min(m, nn);
+    double* Q = t.alloc(m * kmax);
+    double* C = t.alloc(kmax * nn);
+    size_t rank = kmax;
+    if (rank_reduce) rank = qc(t.h, t.core[k], m, nn, Q, C);
+    else qr(t.h, t.core[k], m, nn, Q, C);
+    const size_t ncols = t.cols_right(k + 1);
+    double* nxt = t.alloc(rank * ncols);
+    gemm(t.h, nxt, rank, ncols, 1.0, C, nn, false, nn, t.core[k + 1], ncols, false);
+    t.release(C);
+    t.replace(k, Q);
+    t.replace(k + 1, nxt);
+    t.r[k + 1] = rank;
+}
+
+// transfer_core(k -> k-1): posA = 0 -> CQ (or RQ), posB = last -> prev * R (tensorNetwork.cpp:833-840, 875)
+void transfer_left(TT& t, size_t k, bool rank_reduce) {
+    const size_t m = t.r[k], nn = t.cols_right(k), kmax = std::min(m, nn);
+    double* C = t.alloc(m * kmax);
+    double* Q = t.alloc(kmax * nn);
+    size_t rank = kmax;
+    if (rank_reduce) rank = cq(t.h, t.core[k], m, nn, C, Q);
+    else rq(t.h, t.core[k], m, nn, C, Q);
+    const size_t prow = t.rows_left(k - 1);
+    double* prv = t.alloc(prow * rank);
+    gemm(t.h, prv, prow, rank, 1.0, t.core[k - 1], m, false, m, C, rank, false);
+    t.release(C);
+    t.replace(k, Q);
+    t.replace(k - 1, prv);
+    t.r[k] = rank;
+}
+
+void move_core(TT& t, bool canonicalized, size_t core_pos, size_t pos, bool keep_rank) {
+    const size_t d = t.d;
+    if (canonicalized) {
+        for (size_t k = core_pos; k < pos; ++k) transfer_right(t, k, !keep_rank);
+        for (size_t k = core_pos; k > pos; --k) transfer_left(t, k, !keep_rank);
+    } else {
+        for (size_t k = 0; k < pos; ++k) transfer_right(t, k, !keep_rank);
+        for (size_t k = d - 1; k > pos; --k) transfer_left(t, k, !keep_rank);
+    }
+    while (exceeds_maximal_ranks(t)) {   // ttNetwork.cpp:609-624
+        for (size_t k = pos; k > 0; --k) transfer_left(t, k, !keep_rank);
+        for (size_t k = 0; k + 1 < d; ++k) transfer_right(t, k, !keep_rank);
+        for (size_t k = d - 1; k > pos; --k) transfer_left(t, k, !keep_rank);
+    }
+}
+
+// left-orthogonalise core k into k+1 keeping the rank (round's canonicalisation sweep)
+void orth_right(TT& t, size_t k) {
+    const size_t m = t.rows_left(k), nn = t.r[k + 1];
+    if (m < nn || nn > size_t(kSmallMax)) {  // wide unfolding: rank must drop to m -> reference QC semantics
+        transfer_right(t, k, true);
+        return;
+    }
+    double* Q = t.alloc(m * nn);
+    double* R = t.alloc(nn * nn);
+    orthogonalize(t.h, t.core[k], m, nn, false, Q, R);
+    const size_t ncols = t.cols_right(k + 1);
+    double* nxt = t.alloc(nn * ncols);
+    gemm(t.h, nxt, nn, ncols, 1.0, R, nn, false, nn, t.core[k + 1], ncols, false);
+    t.release(R);
+    t.replace(k, Q);
+    t.replace(k + 1, nxt);
+}
+
+// svd rank cut of calculate_svd (tensor.cpp:1462-1474): max_rank, then first sigma_j <= eps*sigma_0
+size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps) {
+    size_t rank = s.size();
+    if (max_rank != 0) rank = std::min(rank, max_rank);
+    for (size_t j = 1; j < rank; ++j)
+        if (s[j] <= eps * s[0]) return j;
+    return rank;
+}
+
+// truncate the edge between core k-1 and core k (round_edge(k, k-1), core moves to k-1)
+void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
+    const size_t m = t.r[k], nn = t.cols_right(k);
+    const size_t prow = t.rows_left(k - 1);
+    xrs_handle_t h = t.h;
+    if (m <= nn && m <= size_t(kSmallMax)) {
+        double* Q = t.alloc(m * nn);
+        double* L = t.alloc(m * m);
+        const OrthResult o = orthogonalize(h, t.core[k], m, nn, true, Q, L);
+        if (o.certified && eps < 0.5 * o.cert_ratio && max_rank >= m) {
+            double* prv = t.alloc(prow * m);
+            gemm(h, prv, prow, m, 1.0, t.core[k - 1], m, false, m, L, m, false);
+            t.release(L);
+            t.replace(k, Q);
+            t.replace(k - 1, prv);
+            return;
+        }
+        // SVD of the r x r factor: L = U S Vt  ->  B = U S (Vt Q)
+        DevBuf U(h, m * m * 8), S(h, m * 8), Vt(h, m * m * 8);
+        jacobi_svd_rows(h, L, int(m), int(m), U.d(), S.d(), Vt.d());
+        std::vector<double> s(m);
+        XRS_HIP(hipMemcpyAsync(s.data(), S.d(), m * 8, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        const size_t kk = svd_cut(s, max_rank, eps);
+        double* cur = t.alloc(kk * nn);
+        gemm(h, cur, kk, nn, 1.0, Vt.d(), m, false, m, Q, nn, false);          // Vt[:kk] Q
+        scale_cols(h, U.d(), S.d(), m, m);                                     // U S (columns >= kk unused)
+        double* prv = t.alloc(prow * kk);
+        gemm(h, prv, prow, kk, 1.0, t.core[k - 1], m, false, m, U.d(), m, false);  // prev * (U S)[:, :kk]
+        t.release(L);
+        t.release(Q);
+        t.replace(k, cur);
+        t.replace(k - 1, prv);
+        t.r[k] = kk;
+        return;
+    }
+    // tall unfolding (r_k > n_k r_{k+1}) or rank > 512: B = Q R, SVD of R, B = (Q U) S Vt
+    XRS_REQUIRE(nn <= size_t(kSmallMax), "TT round: unfolding with both sides > 512 not supported yet");
+    double* Q = t.alloc(m * nn);
+    double* R = t.alloc(nn * nn);
+    orthogonalize(h, t.core[k], m, nn, false, Q, R);
+    DevBuf U(h, nn * nn * 8), S(h, nn * 8), Vt(h, nn * nn * 8), QU(h, m * nn * 8);
+    jacobi_svd_rows(h, R, int(nn), int(nn), U.d(), S.d(), Vt.d());
+    std::vector<double> s(nn);
+    XRS_HIP(hipMemcpyAsync(s.data(), S.d(), nn * 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    const size_t kk = svd_cut(s, max_rank, eps);
+    double* cur = t.alloc(kk * nn);
+    XRS_HIP(hipMemcpyAsync(cur, Vt.d(), kk * nn * 8, hipMemcpyDeviceToDevice, h->stream));
+    gemm(h, QU.d(), m, nn, 1.0, Q, nn, false, nn, U.d(), nn, false);
+    scale_cols(h, QU.d(), S.d(), m, nn);
+    double* prv = t.alloc(prow * kk);
+    gemm(h, prv, prow, kk, 1.0, t.core[k - 1], m, false, m, QU.d(), nn, false);
+    t.release(Q);
+    t.release(R);
+    t.replace(k, cur);
+    t.replace(k - 1, prv);
+    t.r[k] = kk;
+}
+
+void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, double eps) {
+    const size_t d = t.d;
+    // canonicalize_right (ttNetwork.cpp:638-640, 654)
+    const size_t start = canonicalized ? core_pos : 0;
+    for (size_t k = start; k + 1 < d; ++k) orth_right(t, k);
+    if (!canonicalized)
+        ;  // cores 0..d-2 are now left-orthogonal
+    // right-to-left truncation (ttNetwork.cpp:656-658)
+    for (size_t k = d - 1; k >= 1; --k) truncate_edge(t, k, max_ranks[k - 1], eps);
+}
+
+double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y) {
+    size_t emax = 1, tmax = 1;
+    for (size_t k = 0; k < d; ++k) {
+        emax = std::max(emax, rx[k + 1] * ry[k + 1]);
+        tmax = std::max(tmax, ry[k] * n[k] * rx[k + 1]);
+    }
+    DevBuf E0(h, emax * 8), E1(h, emax * 8), T(h, tmax * 8);
+    const double one = 1.0;
+    XRS_HIP(hipMemcpyAsync(E0.d(), &one, 8, hipMemcpyHostToDevice, h->stream));
+    double* E = E0.d();
+    double* En = E1.d();
+    for (size_t k = 0; k < d; ++k) {
+        const size_t a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+        // T (b x nk a2) = E^T (b x a) * X_k (a x nk a2)
+        gemm(h, T.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);
+        // E' (a2 x b2) = T^T as ((b nk) x a2)^T * Y_k ((b nk) x b2)
+        gemm(h, En, a2, b2, 1.0, T.d(), a2, true, b * nk, Y[k], b2, false);
+        std::swap(E, En);
+    }
+    double* hs = static_cast<double*>(h->host_scratch);
+    XRS_HIP(hipMemcpyAsync(hs, E, 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    return hs[0];
+}
+
+void check_tt(size_t d, const size_t* n, const size_t* r, double* const* cores) {
+    XRS_REQUIRE(d >= 1, "TT must have at least one component");
+    XRS_REQUIRE(n && r && cores, "null TT description");
+    XRS_REQUIRE(r[0] == 1 && r[d] == 1, "boundary ranks must be 1");
+    for (size_t k = 0; k < d; ++k) {
+        XRS_REQUIRE(n[k] > 0 && r[k + 1] > 0, "dimensions and ranks must be positive");
+        XRS_REQUIRE(cores[k] != nullptr, "null core");
+    }
+}
+
+}  // namespace
+
+}  // namespace xrs
+
+using namespace xrs;
+
+extern "C" {
+
+int xrs_tt_move_core(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, int canonicalized,
+                     size_t core_position, size_t position, int keep_rank) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        check_tt(d, n, r, cores);
+        XRS_REQUIRE(position < d, "Illegal core-position");
+        XRS_REQUIRE(!canonicalized || core_position < d, "Illegal current core position");
+        TT t{h, d, n, r, cores};
+        move_core(t, canonicalized != 0, core_position, position, keep_rank != 0);
+    });
+}
+
+int xrs_tt_round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, int canonicalized,
+                 size_t core_position, const size_t* max_ranks, double eps) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        check_tt(d, n, r, cores);
+        XRS_REQUIRE(eps < 1.0 && eps >= 0.0, "_eps must be smaller than one.");
+        for (size_t k = 0; k + 1 < d; ++k)
+            XRS_REQUIRE(max_ranks[k] > 0, "Trying to round a TTTensor to rank 0 is not possible.");
+        XRS_REQUIRE(!canonicalized || core_position < d, "Illegal current core position");
+        TT t{h, d, n, r, cores};
+        round(t, canonicalized != 0, core_position, max_ranks, eps);
+    });
+}
+
+int xrs_tt_dot(xrs_handle_t h, double* result, size_t d, const size_t* n, const size_t* rx, const double* const* X,
+               const size_t* ry, const double* const* Y) {
+    return guarded([&] {
+        XRS_REQUIRE(h && result, "null argument");
+        check_tt(d, n, rx, const_cast<double* const*>(X));
+        check_tt(d, n, ry, const_cast<double* const*>(Y));
+        *result = dot(h, d, n, rx, X, ry, Y);
+    });
+}
+
+}  // extern "C"
