@@ -90,6 +90,35 @@ __global__ void __launch_bounds__(256) k_dev_identity(const double* __restrict__
     }
 }
 
+// First-order second CholeskyQR pass: G2 = I + E with ||E|| tiny -> L2 = I + Elow + O(E^2),
+// Elow = strict_lower(E) + diag(E)/2. Writes L2 (lower) and Linv2 = I - Elow (lower) and max|E|.
+__global__ void __launch_bounds__(256) k_first_order(const double* __restrict__ G2, int n, double* __restrict__ L2,
+                                                     double* __restrict__ Li2, double* __restrict__ emax) {
+    __shared__ double red[4];
+    double mx = 0.0;
+    for (int e = threadIdx.x + blockIdx.x * 256; e < n * n; e += 256 * gridDim.x) {
+        const int i = e / n, j = e % n;
+        const double eij = G2[e] - (i == j ? 1.0 : 0.0);
+        const double d = fabs(eij);
+        mx = (d > mx || d != d) ? d : mx;
+        const double el = (i > j) ? eij : ((i == j) ? 0.5 * eij : 0.0);
+        L2[e] = (i == j ? 1.0 : 0.0) + el;
+        Li2[e] = (i == j ? 1.0 : 0.0) - el;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double t = __shfl_xor(mx, o, 64);
+        mx = (t > mx || t != t) ? t : mx;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = red[0];
+        for (int i = 1; i < 4; ++i) m = (red[i] > m || red[i] != red[i]) ? red[i] : m;
+        emax[blockIdx.x] = m;
+    }
+}
+
 static double max_abs_dev_identity(xrs_handle_t h, const double* G, size_t n) {
     double* out = static_cast<double*>(h->dev_scratch) + 32;
     hipLaunchKernelGGL(k_dev_identity, dim3(1), dim3(256), 0, h->stream, G, int(n), out);
@@ -125,7 +154,7 @@ OrthResult orthogonalize(xrs_handle_t h, const double* A, size_t m, size_t n, bo
     OrthResult res{false, 0.0, false};
     if (N > size_t(kSmallMax)) throw Error{XRS_EINVAL, "orthogonalize: rank > 512 not supported yet"};
     const int Ni = int(N), nvec = int(M);
-    DevBuf G(h, N * N * 8), Dv(h, N * 32 * 8), L1(h, N * N * 8), Q1(h, m * n * 8), st(h, 64);
+    DevBuf G(h, N * N * 8), Dv(h, (N + 32) * 32 * 8), L1(h, N * N * 8), Q1(h, m * n * 8), st(h, 64);
     auto gram = [&](double* out, const double* X) {
         if (wide) gemm(h, out, N, N, 1.0, X, n, false, M, X, n, true);   // X X^T
         else gemm(h, out, N, N, 1.0, X, n, true, M, X, n, false);        // X^T X
@@ -140,6 +169,34 @@ OrthResult orthogonalize(xrs_handle_t h, const double* A, size_t m, size_t n, bo
     potrf(h, G.d(), Ni, -tau_rel, Dv.d(), stv + 0);
     solve(G.d(), A, Q1.d());
     gram(L1.d(), Q1.d());
+    {
+        // second pass: first-order correction when Q1 is already orthonormal to ~1e-8 (then the
+        // neglected O(E^2) term is below u), else a full second Cholesky + TRSM
+        DevBuf L2(h, N * N * 8), Li2(h, N * N * 8);
+        double* emax_dev = static_cast<double*>(h->dev_scratch) + 40;
+        const unsigned nb = 8;
+        hipLaunchKernelGGL(k_first_order, dim3(nb), dim3(256), 0, h->stream, L1.d(), Ni, L2.d(), Li2.d(), emax_dev);
+        check_launch("k_first_order");
+        int* hs = static_cast<int*>(h->host_scratch);
+        double* hd = static_cast<double*>(h->host_scratch) + 8;
+        XRS_HIP(hipMemcpyAsync(hs, stv, 8, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipMemcpyAsync(hd, emax_dev, nb * 8, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        double em = 0.0;
+        for (unsigned i = 0; i < nb; ++i) em = (hd[i] > em || hd[i] != hd[i]) ? hd[i] : em;
+        if (hs[0] == 0 && em <= 1e-8) {
+            if (wide) {
+                gemm(h, Q, N, n, 1.0, Li2.d(), N, false, N, Q1.d(), n, false);      // Q = (I - Elow) Q1
+                gemm(h, RL, N, N, 1.0, G.d(), N, false, N, L2.d(), N, false);      // L = L1 L2
+            } else {
+                gemm(h, Q, m, N, 1.0, Q1.d(), n, false, N, Li2.d(), N, true);      // Q = Q1 (I - Elow)^T
+                gemm(h, RL, N, N, 1.0, L2.d(), N, true, N, G.d(), N, true);        // R = L2^T L1^T
+            }
+            res.certified = true;
+            res.cert_ratio = std::sqrt(0.5 * tau_rel);
+            return res;
+        }
+    }
     potrf(h, L1.d(), Ni, 0.0, Dv.d(), stv + 1);
     solve(L1.d(), Q1.d(), Q);
     if (wide) gemm(h, RL, N, N, 1.0, G.d(), N, false, N, L1.d(), N, false);   // L = L1 L2

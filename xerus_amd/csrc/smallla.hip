@@ -18,7 +18,9 @@
 namespace xrs {
 
 constexpr int NB = 32;
+typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int PMAX = 512;
+constexpr int POT_THREADS = 512;   // 8 waves, two per SIMD: 256 VGPRs for the register-resident 32-wide steps
 
 __device__ __forceinline__ double readlane_d(double v, int l) {
     union { double d; int i[2]; } u;
@@ -29,39 +31,45 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Cholesky
-__global__ void __launch_bounds__(1024) k_potrf(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
+// Cholesky, one workgroup of 1024 threads, 32-wide blocks, right-looking. Per block column:
+//   (1) wave 0 factors the 32x32 diagonal block in registers (lane r owns row r, v_readlane
+//       broadcasts; 64 VGPRs so nothing spills at the 128-VGPR budget of a 1024-thread workgroup);
+//   (2) wave 1 inverts it (D^{-1}, for the TRSM kernel) while the other waves solve the panel rows
+//       x D^T = g by substitution against D in LDS (one row per thread, 32 registers);
+//   (3) all waves apply the rank-32 trailing update from the LDS panel with 4x4 register tiles.
+__global__ void __launch_bounds__(POT_THREADS) k_potrf(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
                                                  int* __restrict__ status, double* __restrict__ info) {
     __shared__ double P[PMAX * (NB + 1)];
     __shared__ double Ds[NB][NB + 1];
-    __shared__ double Dis[NB][NB + 1];
     __shared__ double red[16];
     __shared__ int fail;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    double* dummy = Dinv + size_t(n + 31) * NB + (tid & 31);   // padding row of Dinv: sink for masked stores
     if (tid == 0) fail = 0;
     // trace(G) -> absolute shift (shift_rel * trace), no host round trip
     double tr = 0.0;
-    for (int i = tid; i < n; i += 1024) tr += G[size_t(i) * n + i];
+    for (int i = tid; i < n; i += POT_THREADS) tr += G[size_t(i) * n + i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
     if (lane == 0) red[wave] = tr;
     __syncthreads();
     tr = 0.0;
-    for (int w = 0; w < 16; ++w) tr += red[w];
+    for (int w = 0; w < POT_THREADS / 64; ++w) tr += red[w];
     if (tid == 0 && info) info[0] = tr;
     const double shift = shift_rel * tr;
     if (shift != 0.0)
-        for (int i = tid; i < n; i += 1024) G[size_t(i) * n + i] += shift;
+        for (int i = tid; i < n; i += POT_THREADS) G[size_t(i) * n + i] += shift;
     __syncthreads();
     for (int j0 = 0; j0 < n; j0 += NB) {
         const int jb = min(NB, n - j0);
-        for (int e = tid; e < NB * NB; e += 1024) {
+        for (int e = tid; e < NB * NB; e += POT_THREADS) {
             const int r = e / NB, c = e % NB;
             double v = (r == c) ? 1.0 : 0.0;
             if (r < jb && c < jb && c <= r) v = G[size_t(j0 + r) * n + j0 + c];
             Ds[r][c] = v;
         }
         __syncthreads();
+        // (1) diagonal block: wave 0, lane r holds row r in registers, v_readlane broadcasts
         if (wave == 0) {
             const int r = lane & 31;
             double row[NB];
@@ -75,83 +83,127 @@ __global__ void __launch_bounds__(1024) k_potrf(double* __restrict__ G, int n, d
                 if (!okp && bad == 0 && k < jb) bad = k + 1;
                 if (!okp) dkk = 1.0;
                 const double d = sqrt(dkk);
-                if (r == k) row[k] = d;
-                else if (r > k) row[k] = row[k] / d;
+                const double inv = 1.0 / d;
+                row[k] = (r == k) ? d : ((r > k) ? row[k] * inv : row[k]);
 #pragma unroll
                 for (int l = k + 1; l < NB; ++l) {
                     const double v = readlane_d(row[k], l);
                     if (r >= l) row[l] -= row[k] * v;
                 }
             }
-            // X = D^{-1}: lane c computes column c (lower triangular)
-            double x[NB];
-#pragma unroll
-            for (int i = 0; i < NB; ++i) {
-                double s = (i == r) ? 1.0 : 0.0;
-#pragma unroll
-                for (int k = 0; k < i; ++k) s -= readlane_d(row[k], i) * x[k];
-                x[i] = s / readlane_d(row[i], i);
-            }
             if (lane < 32) {
 #pragma unroll
                 for (int c = 0; c < NB; ++c) Ds[r][c] = (c <= r) ? row[c] : 0.0;
-#pragma unroll
-                for (int i = 0; i < NB; ++i) Dis[i][r] = x[i];
             }
             if (lane == 0 && bad && fail == 0) fail = j0 + bad;
         }
         __syncthreads();
-        for (int e = tid; e < NB * NB; e += 1024) {
-            const int r = e / NB, c = e % NB;
-            if (r < jb && c < jb && c <= r) G[size_t(j0 + r) * n + j0 + c] = Ds[r][c];
-            if (r < jb) Dinv[size_t(j0 + r) * NB + c] = (c < jb) ? Dis[r][c] : 0.0;
-        }
         const int t = n - j0 - jb;
-        if (t > 0) {
-            // panel: P[rr][c] = sum_{k<=c} G[j0+jb+rr][j0+k] * Dinv[c][k]
-            for (int e = tid; e < t * NB; e += 1024) {
-                const int rr = e / NB, c = e % NB;
-                const double* g = G + size_t(j0 + jb + rr) * n + j0;
-                double s = 0.0;
-                for (int k = 0; k <= c && k < jb; ++k) s += g[k] * Dis[c][k];
-                P[rr * (NB + 1) + c] = (c < jb) ? s : 0.0;
-            }
-            __syncthreads();
-            for (int e = tid; e < t * NB; e += 1024) {
-                const int rr = e / NB, c = e % NB;
-                if (c < jb) G[size_t(j0 + jb + rr) * n + j0 + c] = P[rr * (NB + 1) + c];
-            }
-            // trailing lower update with 4x4 register tiles
-            const int T = (t + 3) / 4;
-            for (int e = tid; e < T * T; e += 1024) {
-                const int ti = e / T, tk = e % T;
-                if (tk > ti) continue;
-                double acc[4][4] = {};
-                for (int c = 0; c < jb; ++c) {
-                    double a[4], b[4];
+        if (wave == 1) {
+            // (2a) D^{-1}: lane c computes column c by right-looking substitution in registers.
+            // Stores are unconditional (Dinv is padded to n+32 rows): a runtime-bounded store loop
+            // would make the compiler index x[] dynamically and spill it to scratch.
+            const int c = lane & 31;
+            double x[NB];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int ri = min(4 * ti + u, t - 1), rk = min(4 * tk + u, t - 1);
-                        a[u] = P[ri * (NB + 1) + c];
-                        b[u] = P[rk * (NB + 1) + c];
+            for (int i = 0; i < NB; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+            for (int k = 0; k < NB; ++k) {
+                x[k] = x[k] / Ds[k][k];
+#pragma unroll
+                for (int i = k + 1; i < NB; ++i) x[i] -= Ds[i][k] * x[k];
+            }
+            if (lane < 32) {
+                double* out = Dinv + size_t(j0) * NB + c;
+#pragma unroll
+                for (int i = 0; i < NB; ++i) out[size_t(i) * NB] = x[i];
+            }
+        } else {
+            const int wt = (tid >= 64) ? tid - 64 : tid;   // waves 0, 2, 3, ...
+            for (int e = wt; e < NB * NB; e += POT_THREADS - 64) {
+                const int r = e / NB, c = e % NB;
+                if (r < jb && c < jb && c <= r) G[size_t(j0 + r) * n + j0 + c] = Ds[r][c];
+            }
+            // (2b) panel rows: x D^T = g  <=>  x_c = (g_c - sum_{k<c} x_k D[c][k]) / D[c][c]
+            if (jb == NB) {
+                for (int rr = wt; rr < t; rr += POT_THREADS - 64) {
+                    double* grow = G + size_t(j0 + jb + rr) * n + j0;
+                    // opaque LDS base per iteration: otherwise LICM hoists all 528 loop-invariant D loads
+                    // out of the row loop and spills them
+                    int off = 0;
+                    asm volatile("" : "+v"(off));
+                    const double* D = &Ds[0][0] + off;
+                    double x[NB];
+#pragma unroll
+                    for (int c = 0; c < NB; ++c) x[c] = grow[c];
+#pragma unroll
+                    for (int k = 0; k < NB; ++k) {
+                        x[k] = x[k] / D[k * (NB + 1) + k];
+#pragma unroll
+                        for (int c = k + 1; c < NB; ++c) x[c] -= x[k] * D[c * (NB + 1) + k];
                     }
+                    double* prow = P + rr * (NB + 1);
 #pragma unroll
-                    for (int u = 0; u < 4; ++u)
-#pragma unroll
-                        for (int v = 0; v < 4; ++v) acc[u][v] += a[u] * b[v];
+                    for (int c = 0; c < NB; ++c) {
+                        prow[c] = x[c];
+                        grow[c] = x[c];
+                    }
                 }
-#pragma unroll
-                for (int u = 0; u < 4; ++u)
-#pragma unroll
-                    for (int v = 0; v < 4; ++v) {
-                        const int i = 4 * ti + u, k = 4 * tk + v;
-                        if (i < t && k < t && k <= i) G[size_t(j0 + jb + i) * n + j0 + jb + k] -= acc[u][v];
+            } else {
+                // last partial block: plain loops (rare: only when n is not a multiple of 32)
+                for (int rr = wt; rr < t; rr += POT_THREADS - 64) {
+                    double* grow = G + size_t(j0 + jb + rr) * n + j0;
+                    double* prow = P + rr * (NB + 1);
+                    for (int c = 0; c < NB; ++c) prow[c] = (c < jb) ? grow[c] : 0.0;
+                    for (int k = 0; k < jb; ++k) {
+                        const double xk = prow[k] / Ds[k][k];
+                        prow[k] = xk;
+                        grow[k] = xk;
+                        for (int c = k + 1; c < jb; ++c) prow[c] -= xk * Ds[c][k];
                     }
+                }
+            }
+        }
+        __syncthreads();
+        if (t > 0) {
+            // (3) trailing update G22 -= P P^T on 16x16 tiles with v_mfma_f64_16x16x4_f64 (K = 32 in
+            //     8 steps); one wave per tile, lower tiles only (the strict upper triangle of diagonal
+            //     tiles receives harmless garbage and is zeroed at the end).
+            //     A frag: lane l -> P[i0 + (l&15)][c + (l>>4)]; B frag: P[k0 + (l&15)][c + (l>>4)];
+            //     C/D (f64): row (l>>4) + 4r, col l&15.
+            const int T = (t + 15) / 16;
+            const int ntiles = T * (T + 1) / 2;
+            const int lr = lane & 15, lk = lane >> 4;
+            for (int tile = wave; tile < ntiles; tile += POT_THREADS / 64) {
+                // decode lower-triangular tile index -> (ti, tk), tk <= ti
+                int ti = int((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+                while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+                while (ti * (ti + 1) / 2 > tile) --ti;
+                const int tk = tile - ti * (ti + 1) / 2;
+                const int i0 = ti * 16, k0 = tk * 16;
+                auto cptr = [&](int r) -> double* {
+                    const int i = i0 + lk + 4 * r, k = k0 + lr;
+                    const bool ok = (i < t) && (k < t);
+                    return ok ? (G + size_t(j0 + jb + i) * n + j0 + jb + k) : dummy;
+                };
+                const double cv0 = *cptr(0), cv1 = *cptr(1), cv2 = *cptr(2), cv3 = *cptr(3);
+                d4 acc = {0.0, 0.0, 0.0, 0.0};
+                const int ra = min(i0 + lr, t - 1), rb = min(k0 + lr, t - 1);
+#pragma unroll
+                for (int c = 0; c < NB; c += 4) {
+                    const double av = P[ra * (NB + 1) + c + lk];
+                    const double bv = P[rb * (NB + 1) + c + lk];
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+                }
+                *cptr(0) = cv0 - acc[0];
+                *cptr(1) = cv1 - acc[1];
+                *cptr(2) = cv2 - acc[2];
+                *cptr(3) = cv3 - acc[3];
             }
         }
         __syncthreads();
     }
-    for (int e = tid; e < n * n; e += 1024) {
+    for (int e = tid; e < n * n; e += POT_THREADS) {
         const int r = e / n, c = e % n;
         if (c > r) G[size_t(r) * n + c] = 0.0;
     }
@@ -159,17 +211,19 @@ __global__ void __launch_bounds__(1024) k_potrf(double* __restrict__ G, int n, d
 }
 
 // ---------------------------------------------------------------------------------------------
-// Triangular solve X = L^{-1} Y for 32 right-hand sides per workgroup.
+// Triangular solve X = L^{-1} Y for 32 right-hand sides per workgroup (256 threads). The RHS block
+// lives in LDS as Xs[n][33]; per 32-row block I: T = Y_I - L[I, :i0] X[:i0] (2x2 register tiles,
+// L read through L1) then X_I = Dinv_I T (the diagonal-block inverses from k_potrf).
 template <bool COLS>
 __global__ void __launch_bounds__(256) k_trsm(const double* __restrict__ L, const double* __restrict__ Dinv, int n,
                                               const double* __restrict__ Y, size_t ldy, double* __restrict__ X, size_t ldx,
                                               int nvec) {
     extern __shared__ double Xs[];  // [n][NB + 1]
+    __shared__ double Ts[NB][NB + 1];
     constexpr int S = NB + 1;
     const int tid = threadIdx.x;
     const int v0 = blockIdx.x * NB;
     const int nv = min(NB, nvec - v0);
-    // load RHS block: Xs[i][v] = Y(vector v0+v, entry i)
     for (int e = tid; e < n * NB; e += 256) {
         int i, v;
         if (COLS) { i = e / NB; v = e % NB; } else { v = e / n; i = e % n; }
@@ -178,42 +232,39 @@ __global__ void __launch_bounds__(256) k_trsm(const double* __restrict__ L, cons
         Xs[i * S + v] = y;
     }
     __syncthreads();
-    // thread -> (row r in block, 4 vectors)
-    const int r = tid >> 3;          // 0..31
-    const int vq = (tid & 7) * 4;    // 0,4,...,28
+    // 2x2 tile: rows r0, r0+16 ; vectors c0, c0+16
+    const int r0 = tid >> 4;        // 0..15
+    const int c0 = tid & 15;        // 0..15
     for (int i0 = 0; i0 < n; i0 += NB) {
         const int ib = min(NB, n - i0);
-        double t[4] = {0, 0, 0, 0};
-        if (r < ib) {
-            const double* lrow = L + size_t(i0 + r) * n;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) t[u] = Xs[(i0 + r) * S + vq + u];
+        {
+            const int ra = min(i0 + r0, n - 1), rb = min(i0 + r0 + 16, n - 1);
+            double t00 = Xs[ra * S + c0], t01 = Xs[ra * S + c0 + 16];
+            double t10 = Xs[rb * S + c0], t11 = Xs[rb * S + c0 + 16];
+            const double* la = L + size_t(ra) * n;
+            const double* lb = L + size_t(rb) * n;
             for (int j = 0; j < i0; ++j) {
-                const double l = lrow[j];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) t[u] -= l * Xs[j * S + vq + u];
+                const double a = la[j], b = lb[j];
+                const double x0 = Xs[j * S + c0], x1 = Xs[j * S + c0 + 16];
+                t00 -= a * x0; t01 -= a * x1;
+                t10 -= b * x0; t11 -= b * x1;
             }
+            Ts[r0][c0] = t00; Ts[r0][c0 + 16] = t01;
+            Ts[r0 + 16][c0] = t10; Ts[r0 + 16][c0 + 16] = t11;
         }
         __syncthreads();
-        if (r < ib) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) Xs[(i0 + r) * S + vq + u] = t[u];
-        }
-        __syncthreads();
-        // X_I = Dinv_I * T_I
-        double x[4] = {0, 0, 0, 0};
-        if (r < ib) {
-            const double* drow = Dinv + size_t(i0 + r) * NB;
-            for (int k = 0; k <= r; ++k) {
-                const double dk = drow[k];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) x[u] += dk * Xs[(i0 + k) * S + vq + u];
+        {
+            double x00 = 0, x01 = 0, x10 = 0, x11 = 0;
+            const double* da = Dinv + size_t(min(i0 + r0, n - 1)) * NB;
+            const double* db = Dinv + size_t(min(i0 + r0 + 16, n - 1)) * NB;
+            for (int k = 0; k < NB; ++k) {
+                const double a = da[k], b = db[k];
+                const double t0 = Ts[k][c0], t1 = Ts[k][c0 + 16];
+                x00 += a * t0; x01 += a * t1;
+                x10 += b * t0; x11 += b * t1;
             }
-        }
-        __syncthreads();
-        if (r < ib) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) Xs[(i0 + r) * S + vq + u] = x[u];
+            if (r0 < ib) { Xs[(i0 + r0) * S + c0] = x00; Xs[(i0 + r0) * S + c0 + 16] = x01; }
+            if (r0 + 16 < ib) { Xs[(i0 + r0 + 16) * S + c0] = x10; Xs[(i0 + r0 + 16) * S + c0 + 16] = x11; }
         }
         __syncthreads();
     }
@@ -530,7 +581,7 @@ __global__ void __launch_bounds__(1024) k_svd_finish(const double* __restrict__ 
 void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int* status_dev, double* info_dev) {
     XRS_REQUIRE(n >= 1 && n <= PMAX, "potrf: n out of range for the single-workgroup kernel");
     KernelTimer timer(h, XRS_KFAM_QR, double(n) * n * n / 3.0, 16.0 * double(n) * n);
-    hipLaunchKernelGGL(k_potrf, dim3(1), dim3(1024), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
+    hipLaunchKernelGGL(k_potrf, dim3(1), dim3(POT_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
     check_launch("k_potrf");
 }
 
@@ -542,8 +593,8 @@ void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n,
     const size_t lds = size_t(n) * (NB + 1) * sizeof(double);
     static bool attr_set = false;
     if (!attr_set) {
-        XRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm<false>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        XRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm<true>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        XRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm<false>), hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024));
+        XRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm<true>), hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024));
         attr_set = true;
     }
     const unsigned blocks = unsigned((nvec + NB - 1) / NB);
