@@ -1,0 +1,77 @@
+// TensorNetwork: graph of tensors connected by links (reference include/xerus/tensorNetwork.h:50-574).
+// Used by the indexed-expression engine; pairwise contraction = (at most one) permutation + one GEMM on
+// the GPU (tensorNetwork.cpp:1037-1229), multi-node contraction order from the reference's greedy
+// heuristics with cost m*n*r (contractionHeuristic.cpp:35-381).
+#pragma once
+#include <memory>
+#include <set>
+#include <vector>
+
+#include "tensor.h"
+
+namespace xerus {
+
+class TensorNetwork {
+   public:
+    struct Link {
+        size_t other;           // node id, or (for external links) the external index position
+        size_t indexPosition;   // position of the mode in the other node (or external slot)
+        size_t dimension;
+        bool external;
+        Link() = default;
+        Link(size_t _other, size_t _indexPos, size_t _dim, bool _external)
+            : other(_other), indexPosition(_indexPos), dimension(_dim), external(_external) {}
+        bool links(size_t _other) const { return !external && other == _other; }
+    };
+    struct TensorNode {
+        std::unique_ptr<Tensor> tensorObject;
+        std::vector<Link> neighbors;
+        bool erased = false;
+        TensorNode() = default;
+        TensorNode(std::unique_ptr<Tensor>&& _t, std::vector<Link> _n) : tensorObject(std::move(_t)), neighbors(std::move(_n)) {}
+        TensorNode(const TensorNode& _o)
+            : tensorObject(_o.tensorObject ? new Tensor(*_o.tensorObject) : nullptr), neighbors(_o.neighbors), erased(_o.erased) {}
+        TensorNode(TensorNode&&) = default;
+        TensorNode& operator=(const TensorNode& _o) {
+            tensorObject.reset(_o.tensorObject ? new Tensor(*_o.tensorObject) : nullptr);
+            neighbors = _o.neighbors;
+            erased = _o.erased;
+            return *this;
+        }
+        TensorNode& operator=(TensorNode&&) = default;
+        size_t degree() const { return neighbors.size(); }
+    };
+
+    std::vector<size_t> dimensions;        // external dimensions
+    std::vector<TensorNode> nodes;
+    std::vector<Link> externalLinks;       // external slot -> (node, mode)
+
+    TensorNetwork();
+    explicit TensorNetwork(Tensor _tensor);
+    TensorNetwork(const TensorNetwork&) = default;
+    TensorNetwork(TensorNetwork&&) = default;
+    TensorNetwork& operator=(const TensorNetwork&) = default;
+    TensorNetwork& operator=(TensorNetwork&&) = default;
+
+    size_t degree() const { return dimensions.size(); }
+    size_t num_nodes() const;
+    /// Contracts nodes id1 and id2 into id1 (id2 erased); GPU permutation + GEMM.
+    void contract(const size_t _nodeId1, const size_t _nodeId2);
+    /// Contracts a set of nodes (greedy heuristics for > 3 nodes) and returns the remaining node id.
+    size_t contract(const std::set<size_t>& _ids);
+    /// Full contraction to a dense tensor in external-index order.
+    Tensor to_tensor() const;
+    value_t frob_norm() const;
+    /// Estimated flops (m*n*r) of contracting everything in the heuristic's order.
+    double contraction_cost(const std::set<size_t>& _ids) const;
+
+    void require_valid_network() const;
+    void sanitize();   // drop erased nodes, renumber
+};
+
+namespace internal {
+/// best greedy contraction order over the reference's five score functions (contractionHeuristic.cpp)
+std::vector<std::pair<size_t, size_t>> greedy_contraction_order(const TensorNetwork& _net, double* _cost = nullptr);
+}  // namespace internal
+
+}  // namespace xerus

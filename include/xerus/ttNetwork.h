@@ -1,0 +1,134 @@
+// TTTensor (= TTNetwork<false>) for the MI355X build: the cores stay in HBM; move_core, round,
+// frob_norm and <x,y> run on the GPU (xerus_amd TT drivers).
+// API surface of the reference's TTNetwork (include/xerus/ttNetwork.h:46-519, src/xerus/ttNetwork.cpp).
+#pragma once
+#include <vector>
+
+#include "tensor.h"
+
+namespace xerus {
+
+class TTTensor;
+template <>
+class IndexedTensor<TTTensor>;
+
+class TTTensor {
+   public:
+    /// component k has dims (r_k, n_k, r_{k+1}), r_0 = r_d = 1 (ttNetwork.cpp:57-108)
+    std::vector<Tensor> components;
+    std::vector<size_t> dimensions;
+    bool canonicalized = false;
+    size_t corePosition = 0;
+
+    TTTensor();
+    /// all-zero TT of rank 1 (ttNetwork.cpp:57-108)
+    explicit TTTensor(const Tensor::DimensionTuple& _dimensions);
+    explicit TTTensor(size_t _degree);
+    /// TT-SVD of a dense tensor (ttNetwork.cpp:111-160)
+    explicit TTTensor(const Tensor& _tensor, const double _eps = EPSILON,
+                      const size_t _maxRank = std::numeric_limits<size_t>::max());
+    TTTensor(const Tensor& _tensor, const double _eps, const std::vector<size_t>& _maxRanks);
+
+    /// raw N(0,1) cores of the capped ranks (reduce_to_maximal_ranks), then move_core(0) (ttNetwork.h:129-157)
+    template <class distribution = std::normal_distribution<value_t>, class generator = std::mt19937_64>
+    static TTTensor random(std::vector<size_t> _dimensions, const std::vector<size_t>& _ranks,
+                           distribution& _dist = misc::defaultNormalDistribution, generator& _rnd = misc::randomEngine) {
+        TTTensor result = random_raw(_dimensions, _ranks, _dist, _rnd);
+        result.move_core(0);
+        return result;
+    }
+    template <class distribution = std::normal_distribution<value_t>, class generator = std::mt19937_64>
+    static TTTensor random(std::vector<size_t> _dimensions, const size_t _rank,
+                           distribution& _dist = misc::defaultNormalDistribution, generator& _rnd = misc::randomEngine) {
+        return random(_dimensions, std::vector<size_t>(_dimensions.empty() ? 0 : _dimensions.size() - 1, _rank), _dist, _rnd);
+    }
+    template <class distribution = std::normal_distribution<value_t>, class generator = std::mt19937_64>
+    static TTTensor random_raw(std::vector<size_t> _dimensions, const std::vector<size_t>& _ranks,
+                               distribution& _dist = misc::defaultNormalDistribution, generator& _rnd = misc::randomEngine) {
+        XERUS_REQUIRE(_ranks.size() + 1 == _dimensions.size(), "Non-matching amount of ranks given to TTNetwork::random.");
+        const std::vector<size_t> target = reduce_to_maximal_ranks(_ranks, _dimensions);
+        TTTensor result(_dimensions.size());
+        result.dimensions = _dimensions;
+        const size_t d = _dimensions.size();
+        for (size_t i = 0; i < d; ++i) {
+            const size_t l = (i == 0) ? 1 : target[i - 1];
+            const size_t r = (i + 1 == d) ? 1 : target[i];
+            result.components[i] = Tensor::random({l, _dimensions[i], r}, _dist, _rnd);
+        }
+        result.canonicalized = false;
+        return result;
+    }
+    static std::vector<size_t> reduce_to_maximal_ranks(std::vector<size_t> _ranks, const std::vector<size_t>& _dimensions);
+
+    size_t degree() const { return dimensions.size(); }
+    std::vector<size_t> ranks() const;
+    size_t rank(const size_t _i) const;
+    const Tensor& get_component(const size_t _idx) const { return components.at(_idx); }
+    Tensor& component(const size_t _idx);
+    void set_component(const size_t _idx, Tensor _T);
+    bool exceeds_maximal_ranks() const;
+
+    void move_core(const size_t _position, const bool _keepRank = false);
+    void canonicalize_left() { move_core(0); }
+    void canonicalize_right() { move_core(degree() == 0 ? 0 : degree() - 1); }
+    void assume_core_position(const size_t _pos);
+
+    void round(const std::vector<size_t>& _maxRanks, const double _eps = EPSILON);
+    void round(const size_t _maxRank);
+    void round(const int _maxRank);
+    void round(const value_t _eps);
+
+    value_t frob_norm() const;
+
+    TTTensor& operator+=(const TTTensor& _other);
+    TTTensor& operator-=(const TTTensor& _other);
+    TTTensor& operator*=(const value_t _factor);
+    TTTensor& operator/=(const value_t _divisor);
+
+    /// full contraction to a dense tensor
+    operator Tensor() const;
+    Tensor to_tensor() const;
+
+    IndexedTensor<TTTensor> operator()(const std::vector<Index>& _indices) const;
+    template <typename... args>
+    IndexedTensor<TTTensor> operator()(args... _args) const;
+
+    void require_correct_format() const;
+};
+
+TTTensor operator+(TTTensor _lhs, const TTTensor& _rhs);
+TTTensor operator-(TTTensor _lhs, const TTTensor& _rhs);
+TTTensor operator*(const value_t _factor, TTTensor _tt);
+TTTensor operator*(TTTensor _tt, const value_t _factor);
+TTTensor operator/(TTTensor _tt, const value_t _divisor);
+inline value_t frob_norm(const TTTensor& _tt) { return _tt.frob_norm(); }
+/// <x, y> on the GPU (left-to-right zipper, no permutations)
+value_t dot(const TTTensor& _x, const TTTensor& _y);
+bool approx_equal(const TTTensor& _a, const TTTensor& _b, const value_t _eps = EPSILON);
+
+/// Indexed TT, supporting the full contraction value_t(x(i&0) * y(i&0)) of the reference.
+template <>
+class IndexedTensor<TTTensor> {
+   public:
+    const TTTensor* tt;
+    std::vector<Index> indices;
+};
+
+class IndexedTTProduct {
+   public:
+    const TTTensor* x;
+    const TTTensor* y;
+    std::vector<Index> ix, iy;
+    value_t scale = 1.0;
+    operator value_t() const;
+};
+IndexedTTProduct operator*(const IndexedTensor<TTTensor>& _a, const IndexedTensor<TTTensor>& _b);
+
+template <typename... args>
+IndexedTensor<TTTensor> TTTensor::operator()(args... _args) const {
+    return (*this)(std::vector<Index>({Index(_args)...}));
+}
+
+using TTNetwork = TTTensor;
+
+}  // namespace xerus

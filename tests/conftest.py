@@ -40,3 +40,14 @@ def ref():
     from oracle import xerus_ref
 
     return xerus_ref
+
+
+@pytest.fixture(scope="session")
+def xe():
+    """The C++ host API (pybind module over libxerus_amd); GPU only."""
+    if not _gpu_available():
+        pytest.skip("no GPU visible")
+    import xerus_amd.xerus as module
+
+    module.seed(0xBAADF00D)
+    return module

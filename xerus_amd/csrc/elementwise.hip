@@ -129,6 +129,124 @@ void scale_cols(xrs_handle_t h, double* X, const double* s, size_t m, size_t n) 
     check_launch("k_scale_cols");
 }
 
+// out[p] = sum_i X[p][i][i]  (trace of the two trailing modes, Tensor::perform_trace tensor.cpp:781-838)
+__global__ void __launch_bounds__(256) k_diag_sum(double* __restrict__ out, const double* __restrict__ X, size_t P, size_t m) {
+    const size_t stride = size_t(gridDim.x) * blockDim.x;
+    for (size_t p = size_t(blockIdx.x) * blockDim.x + threadIdx.x; p < P; p += stride) {
+        const double* x = X + p * m * m;
+        double s = 0.0;
+        for (size_t i = 0; i < m; ++i) s += x[i * m + i];
+        out[p] = s;
+    }
+}
+
+void diag_sum(xrs_handle_t h, double* out, const double* X, size_t P, size_t m) {
+    if (!P) return;
+    KernelTimer timer(h, XRS_KFAM_ELEMWISE, double(P * m), 8.0 * double(P * (m + 1)));
+    hipLaunchKernelGGL(k_diag_sum, dim3(ew_blocks(P)), dim3(256), 0, h->stream, out, X, P, m);
+    check_launch("k_diag_sum");
+}
+
+// out[offsets + idx] += alpha * in[idx] for every multi-index idx of `in` (Tensor::offset_add, tensor.cpp:969-1025)
+struct OffsetArgs {
+    int nd;
+    size_t in_dims[16];
+    size_t out_str[16];
+    size_t base;
+};
+__global__ void __launch_bounds__(256) k_offset_add(double* __restrict__ out, const double* __restrict__ in, size_t total,
+                                                    double alpha, OffsetArgs a) {
+    const size_t stride = size_t(gridDim.x) * blockDim.x;
+    for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+        size_t rem = i, off = a.base;
+        for (int k = a.nd - 1; k >= 0; --k) {
+            off += (rem % a.in_dims[k]) * a.out_str[k];
+            rem /= a.in_dims[k];
+        }
+        out[off] += alpha * in[i];
+    }
+}
+
+void offset_add(xrs_handle_t h, double* out, const size_t* out_dims, const double* in, const size_t* in_dims, size_t nd,
+                const size_t* offsets, double alpha) {
+    XRS_REQUIRE(nd <= 16, "offset_add: too many modes");
+    OffsetArgs a{};
+    a.nd = int(nd);
+    size_t total = 1, s = 1;
+    a.base = 0;
+    for (int k = int(nd) - 1; k >= 0; --k) {
+        a.in_dims[k] = in_dims[k];
+        a.out_str[k] = s;
+        a.base += offsets[k] * s;
+        s *= out_dims[k];
+        total *= in_dims[k];
+    }
+    if (!total) return;
+    KernelTimer timer(h, XRS_KFAM_ELEMWISE, double(total), 24.0 * double(total));
+    hipLaunchKernelGGL(k_offset_add, dim3(ew_blocks(total)), dim3(256), 0, h->stream, out, in, total, alpha, a);
+    check_launch("k_offset_add");
+}
+
+// Generalised evaluation (internal::evaluate, indexedTensor_tensor_evaluate.cpp:248-390):
+// out[o] = sum_{t} in[base + sum_k o_k*in_str[k] + sum_j t_j*tr_str[j]], o over out_dims, t over tr_dims.
+// Covers fixed indices (base offset), traces (tr_*) and diagonals in one pass; plain permutations use the
+// LDS-tiled permute instead. One thread per output element, consecutive threads walk the last out mode.
+struct EvalArgs {
+    int nd, nt;
+    size_t out_dims[24];
+    size_t in_str[24];
+    size_t tr_dims[12];
+    size_t tr_str[12];
+    size_t base;
+    size_t tr_total;
+};
+__global__ void __launch_bounds__(256) k_strided_eval(double* __restrict__ out, const double* __restrict__ in, size_t total,
+                                                      EvalArgs a) {
+    const size_t stride = size_t(gridDim.x) * blockDim.x;
+    for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < total; i += stride) {
+        size_t rem = i, off = a.base;
+        for (int k = a.nd - 1; k >= 0; --k) {
+            off += (rem % a.out_dims[k]) * a.in_str[k];
+            rem /= a.out_dims[k];
+        }
+        double s = 0.0;
+        for (size_t t = 0; t < a.tr_total; ++t) {
+            size_t r = t, o2 = off;
+            for (int j = a.nt - 1; j >= 0; --j) {
+                o2 += (r % a.tr_dims[j]) * a.tr_str[j];
+                r /= a.tr_dims[j];
+            }
+            s += in[o2];
+        }
+        out[i] = s;
+    }
+}
+
+void strided_eval(xrs_handle_t h, double* out, const double* in, size_t nd, const size_t* out_dims, const size_t* in_strides,
+                  size_t nt, const size_t* tr_dims, const size_t* tr_strides, size_t base) {
+    XRS_REQUIRE(nd <= 24 && nt <= 12, "strided_eval: too many modes");
+    EvalArgs a{};
+    a.nd = int(nd);
+    a.nt = int(nt);
+    a.base = base;
+    size_t total = 1;
+    for (size_t k = 0; k < nd; ++k) {
+        a.out_dims[k] = out_dims[k];
+        a.in_str[k] = in_strides[k];
+        total *= out_dims[k];
+    }
+    a.tr_total = 1;
+    for (size_t j = 0; j < nt; ++j) {
+        a.tr_dims[j] = tr_dims[j];
+        a.tr_str[j] = tr_strides[j];
+        a.tr_total *= tr_dims[j];
+    }
+    if (!total) return;
+    KernelTimer timer(h, XRS_KFAM_PERMUTE, double(total * a.tr_total), 8.0 * double(total * (a.tr_total + 1)));
+    hipLaunchKernelGGL(k_strided_eval, dim3(ew_blocks(total)), dim3(256), 0, h->stream, out, in, total, a);
+    check_launch("k_strided_eval");
+}
+
 }  // namespace xrs
 
 using namespace xrs;

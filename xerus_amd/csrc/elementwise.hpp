@@ -13,6 +13,11 @@ void scal(xrs_handle_t h, double* x, double alpha, size_t n);
 void axpy(xrs_handle_t h, double* y, double alpha, const double* x, size_t n);
 void scale_rows(xrs_handle_t h, double* X, const double* s, size_t m, size_t n);
 void scale_cols(xrs_handle_t h, double* X, const double* s, size_t m, size_t n);
+void diag_sum(xrs_handle_t h, double* out, const double* X, size_t P, size_t m);
+void offset_add(xrs_handle_t h, double* out, const size_t* out_dims, const double* in, const size_t* in_dims, size_t nd,
+                const size_t* offsets, double alpha);
+void strided_eval(xrs_handle_t h, double* out, const double* in, size_t nd, const size_t* out_dims, const size_t* in_strides,
+                  size_t nt, const size_t* tr_dims, const size_t* tr_strides, size_t base);
 
 // gemm.hip
 void gemm(xrs_handle_t h, double* C, size_t M, size_t N, double alpha, const double* A, size_t lda, bool ta, size_t K,

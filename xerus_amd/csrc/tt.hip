@@ -253,6 +253,25 @@ void check_tt(size_t d, const size_t* n, const size_t* r, double* const* cores) 
 
 }  // namespace
 
+namespace tt {
+void move_core(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
+               size_t pos, bool keep_rank) {
+    check_tt(d, n, r, cores);
+    TT t{h, d, n, r, cores};
+    xrs::move_core(t, canonicalized, core_pos, pos, keep_rank);
+}
+void round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
+           const size_t* max_ranks, double eps) {
+    check_tt(d, n, r, cores);
+    TT t{h, d, n, r, cores};
+    xrs::round(t, canonicalized, core_pos, max_ranks, eps);
+}
+double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y) {
+    return xrs::dot(h, d, n, rx, X, ry, Y);
+}
+}  // namespace tt
+
 }  // namespace xrs
 
 using namespace xrs;

@@ -1,0 +1,15 @@
+// C++-level entry points of the TT drivers (tt.hip) for the xerus host API. Cores are device buffers of
+// the handle's pool; functions that change ranks release the old cores and allocate new ones.
+#pragma once
+#include "runtime.hpp"
+
+namespace xrs {
+namespace tt {
+void move_core(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
+               size_t pos, bool keep_rank);
+void round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
+           const size_t* max_ranks, double eps);
+double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y);
+}  // namespace tt
+}  // namespace xrs
