@@ -57,7 +57,8 @@ def test_qc_cq_rank_deficient_matches_reference_rule(handle, ref, m, n, k, sign)
     assert _rel(Cc.numpy() @ Qc.numpy(), A) <= 1e-11
 
 
-@pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (400, 128), (5120, 256), (128, 2560), (33, 700)])
+@pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (400, 128), (5120, 256), (128, 2560), (33, 700), (2000, 250),
+                                 (1500, 33), (100, 3000), (1200, 300), (300, 1200), (6000, 512), (512, 4000)])
 def test_qr_rq(handle, m, n):
     A = np.random.default_rng(m + 3 * n).standard_normal((m, n))
     k = min(m, n)
@@ -93,3 +94,14 @@ def test_svd_rank_deficient(handle, ref):
     _, Sr, _ = ref.svd(A)
     assert ref.svd_rank(Sh, 0, ref.EPSILON) == ref.svd_rank(Sr, 0, ref.EPSILON) == 6
     assert np.max(np.abs(Sh - Sr)) <= 1e-12 * Sr[0]
+
+
+@pytest.mark.parametrize("m,n,scale", [(3000, 200, 1e-6), (2000, 256, 1e6), (1000, 96, 1e-3)])
+def test_qr_graded_columns(handle, m, n, scale):
+    """Columns graded over `scale` (kappa ~ 1/scale or scale): CholeskyQR2 path + its certification and fallback."""
+    rng = np.random.default_rng(m + n)
+    A = rng.standard_normal((m, n)) * np.logspace(0, np.log10(scale), n)[None, :]
+    Q, R = handle.qr(handle.array(A))
+    Qh, Rh = Q.numpy(), R.numpy()
+    assert _rel(Qh @ Rh, A) <= 1e-12
+    assert np.linalg.norm(Qh.T @ Qh - np.eye(n)) <= TOL * n

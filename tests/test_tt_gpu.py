@@ -129,6 +129,47 @@ def test_round_sum_recovers_ranks(handle, ref):
     assert diff <= 1e-10 * nrm
 
 
+@pytest.mark.parametrize("edge", [1, 3])
+def test_round_certificate_fails_mid_sweep(handle, ref, edge):
+    """The right unfolding of one interior core is rank-deficient: the certified right-to-left sweep
+    (ranks within maxRank, left Grams well conditioned) must hand over to the reference's two-sweep
+    algorithm at that edge and reproduce the reference's rank drop."""
+    rng = ref.Rng(19)
+    dims, ranks = [5, 5, 5, 5, 5], [4, 6, 6, 4]
+    x = ref.TT.random_raw(dims, ranks, rng)
+    c = x.cores[edge]
+    a = c.shape[0]
+    M = c.reshape(a, -1)
+    U, S, Vt = np.linalg.svd(M, full_matrices=False)
+    S[2:] = 0.0
+    x.cores[edge] = ((U * S) @ Vt).reshape(c.shape)
+    g = capi.TTDevice.from_cores(handle, [cc.copy() for cc in x.cores])
+    y = x.copy()
+    y.round(6)
+    g.round(6)
+    assert g.ranks == y.ranks
+    assert g.ranks[edge - 1] == 2   # internal ranks: bond (edge-1, edge)
+    diff, nrm = _tt_diff_norm(ref, g.cores(), x.cores)
+    assert diff <= 1e-10 * nrm
+
+
+def test_round_bench_shape(handle, ref):
+    """The benched configuration (order 10, n = 20, rank 256): certified path, exact ranks, same tensor."""
+    rng = ref.Rng(23)
+    x = ref.TT.random_raw([20] * 10, [256] * 9, rng)
+    g = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    g.move_core(0)
+    r0 = g.ranks
+    g.round(256)
+    assert g.ranks == r0
+    gc = g.cores()
+    for c in gc[1:]:
+        M = c.reshape(c.shape[0], -1)
+        assert np.linalg.norm(M @ M.T - np.eye(M.shape[0])) <= 1e-12 * M.shape[0]
+    diff, nrm = _tt_diff_norm(ref, gc, x.cores)
+    assert diff <= 1e-10 * nrm
+
+
 def test_tt_errors(handle, ref):
     rng = ref.Rng(1)
     x = ref.TT.random([3, 3, 3], [2, 2], rng)

@@ -211,69 +211,375 @@ __global__ void __launch_bounds__(POT_THREADS) k_potrf(double* __restrict__ G, i
 }
 
 // ---------------------------------------------------------------------------------------------
-// Triangular solve X = L^{-1} Y for 32 right-hand sides per workgroup (256 threads). The RHS block
-// lives in LDS as Xs[n][33]; per 32-row block I: T = Y_I - L[I, :i0] X[:i0] (2x2 register tiles,
-// L read through L1) then X_I = Dinv_I T (the diagonal-block inverses from k_potrf).
-template <bool COLS>
-__global__ void __launch_bounds__(256) k_trsm(const double* __restrict__ L, const double* __restrict__ Dinv, int n,
-                                              const double* __restrict__ Y, size_t ldy, double* __restrict__ X, size_t ldx,
-                                              int nvec) {
-    extern __shared__ double Xs[];  // [n][NB + 1]
-    __shared__ double Ts[NB][NB + 1];
-    constexpr int S = NB + 1;
-    const int tid = threadIdx.x;
-    const int v0 = blockIdx.x * NB;
-    const int nv = min(NB, nvec - v0);
-    for (int e = tid; e < n * NB; e += 256) {
-        int i, v;
-        if (COLS) { i = e / NB; v = e % NB; } else { v = e / n; i = e % n; }
-        double y = 0.0;
-        if (v < nv) y = COLS ? Y[size_t(i) * ldy + v0 + v] : Y[size_t(v0 + v) * ldy + i];
-        Xs[i * S + v] = y;
+// Register-resident Cholesky for n <= 256, one workgroup of 8 waves. The lower triangle of G lives
+// in the MFMA accumulator layout of 16x16 tiles (tile t of the column-major lower enumeration
+// belongs to wave t % 8, slot t / 8; <= 17 tiles = 136 VGPRs per lane), so the right-looking sweep
+// never touches HBM/L2 between the initial load and the final store. Per 16-column block j:
+//   (A) the owner of tile (j,j) publishes it to LDS;
+//   (B) wave 0 factors it in registers (lane r owns row r of the symmetric Schur complement, so
+//       column k of L is lane k's row: v_readlane broadcasts, rsqrt + Newton) and inverts it
+//       (lane c forward-substitutes column c); the inverse also goes to Dinv for the TRSM;
+//   (C) owners of the panel tiles form L_ij = G_ij L_jj^{-T} with 4 fp64 MFMAs and publish them;
+//   (D) every wave applies G_ik -= L_ij L_kj^T to its trailing tiles (4 MFMAs per tile).
+constexpr int PR_THREADS = 512;
+constexpr int PR_WAVES = PR_THREADS / 64;
+constexpr int PR_TMAX = 16;
+constexpr int PR_SLOTS = (PR_TMAX * (PR_TMAX + 1) / 2 + PR_WAVES - 1) / PR_WAVES;
+constexpr int PT = 17;           // LDS row stride of a 16x16 tile (conflict-free MFMA operand reads)
+constexpr int PTILE = 16 * PT;
+
+__device__ __forceinline__ double rsqrt_nr(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double e = fma(-x * y, y, 1.0);   // 1 - x y^2
+        y = fma(0.5 * y, e, y);
+    }
+    return y;
+}
+
+// Wave-level ordering of LDS traffic between lanes of one wave (LDS executes a wave's ops in order).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifdef XRS_POTRF_STAMPS
+__device__ long long* g_potrf_stamps;
+#define PSTAMP(i) do { if (threadIdx.x == 0) g_potrf_stamps[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define PSTAMP(i) do { } while (0)
+#endif
+// Broadcast lane k of every 16-lane row to the whole row (DPP row_newbcast, gfx90a+): one VALU op per
+// dword, no SGPR round trip.
+template <int K>
+__device__ __forceinline__ double row_bcast_d(double v) {
+    union { double d; int i[2]; } u;
+    u.d = v;
+    u.i[0] = __builtin_amdgcn_update_dpp(0, u.i[0], 0x150 + K, 0xF, 0xF, false);
+    u.i[1] = __builtin_amdgcn_update_dpp(0, u.i[1], 0x150 + K, 0xF, 0xF, false);
+    return u.d;
+}
+
+template <int K>
+__device__ __forceinline__ void factor_step(double (&a)[16], double* ivs, int lane, int valid, int& bad) {
+    double dkk = row_bcast_d<K>(a[K]);
+    const bool ok = (dkk > 0.0) && (dkk < 1.0e300);   // rejects <= 0, NaN and Inf
+    if (!ok && bad == 0 && K < valid) bad = K + 1;
+    if (!ok) dkk = 1.0;
+    const double v = rsqrt_nr(dkk);
+    if (lane == 0) ivs[K] = v;
+    const double lrk = a[K] * v;                       // L_rk (r > k); sqrt(dkk) for r == k
+    const double nl = -lrk * v;
+#pragma unroll
+    for (int l = K + 1; l < 16; ++l) a[l] = fma(nl, row_bcast_d<K>(a[l]), a[l]);
+    a[K] = lrk;
+}
+
+template <int K>
+__device__ __forceinline__ void factor_all(double (&a)[16], double* ivs, int lane, int valid, int& bad) {
+    if constexpr (K < 16) {
+        factor_step<K>(a, ivs, lane, valid, bad);
+        factor_all<K + 1>(a, ivs, lane, valid, bad);
+    }
+}
+
+// (B): factor the 16x16 tile in Dt (full symmetric), leave L_jj (lower, zero upper) in Dt and
+// L_jj^{-1} in Di and dinv_out (row-major 16x16). Returns 1 + first failing local column or 0.
+// Every 16-lane row of wave 0 factors the tile redundantly (lane r & 15 owns row r of the Schur
+// complement; column k of L is lane k's row, broadcast with DPP row_newbcast).
+__device__ __forceinline__ int diag_factor16(double* Dt, double* Di, double* ivs, double* __restrict__ dinv_out,
+                                             int lane, int valid) {
+    const int r = lane & 15;
+    double a[16];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) a[c] = Dt[r * PT + c];
+    int bad = 0;
+    factor_all<0>(a, ivs, lane, valid, bad);
+    if (lane < 16) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) Dt[r * PT + c] = (c <= r) ? a[c] : 0.0;
+    }
+    wave_lds_sync();
+#ifdef XRS_POTRF_STAMPS
+    if (lane == 0) g_potrf_stamps[1000 + blockIdx.x] = __builtin_amdgcn_s_memtime();
+#endif
+    // column c of L^{-1}, right-looking (dependency chain of 2 ops per k): x_k *= 1/L_kk, x_i -= L_ik x_k
+    const int c = lane & 15;
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        x[k] *= ivs[k];
+#pragma unroll
+        for (int i = k + 1; i < 16; ++i) x[i] = fma(-Dt[i * PT + k], x[k], x[i]);
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            Di[i * PT + c] = x[i];
+            dinv_out[i * 16 + c] = x[i];
+        }
+    }
+    return bad;
+}
+
+__device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
+                                              int* __restrict__ status, double* __restrict__ info) {
+    __shared__ double Dt[PTILE];
+    __shared__ double Di[PTILE];
+    __shared__ double P[PR_TMAX * PTILE];
+    __shared__ double ivs[16];
+    __shared__ double red[PR_WAVES];
+    __shared__ int fail;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lg = lane >> 4;
+    const int T = (n + 15) >> 4;
+    const int ntiles = T * (T + 1) / 2;
+    if (tid == 0) fail = 0;
+    PSTAMP(0);
+    double tr = 0.0;
+    for (int i = tid; i < n; i += PR_THREADS) tr += G[size_t(i) * n + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
+    if (lane == 0) red[wave] = tr;
+    __syncthreads();
+    tr = 0.0;
+#pragma unroll
+    for (int w = 0; w < PR_WAVES; ++w) tr += red[w];
+    if (tid == 0 && info) info[0] = tr;
+    const double shift = shift_rel * tr;
+
+    // tile ownership + load (identity padding beyond n)
+    int ti[PR_SLOTS], tk[PR_SLOTS];
+    d4 acc[PR_SLOTS];
+#pragma unroll
+    for (int s = 0; s < PR_SLOTS; ++s) {
+        const int t = s * PR_WAVES + wave;
+        int i = -1, k = -1;
+        if (t < ntiles) {
+            int start = 0;
+            k = 0;
+            while (t >= start + (T - k)) { start += T - k; ++k; }
+            i = k + (t - start);
+        }
+        ti[s] = i;
+        tk[s] = k;
+        // unconditional loads from clamped addresses (no load-dependent arithmetic under a branch, so
+        // all 4*PR_SLOTS loads are in flight together); padding / shift fixed up below
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = min(max(16 * i + lg + 4 * q, 0), n - 1), col = min(max(16 * k + lr, 0), n - 1);
+            acc[s][q] = G[size_t(row) * n + col];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < PR_SLOTS; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 16 * ti[s] + lg + 4 * q, col = 16 * tk[s] + lr;
+            const bool inside = ti[s] >= 0 && row < n && col < n;
+            const double pad = (row == col) ? 1.0 : 0.0;
+            acc[s][q] = inside ? acc[s][q] + ((row == col) ? shift : 0.0) : pad;
+        }
+
+    for (int j = 0; j < T; ++j) {
+        // lane offsets made opaque per iteration: otherwise LICM hoists one LDS address per slot out of
+        // the j loop and the 17 accumulator tiles spill
+        int oc = (lg * PT + lr) * 8, oa = (lr * PT + lg) * 8;
+        asm volatile("" : "+v"(oc), "+v"(oa));
+        auto cpos = [&](double* base, int q) -> double* {   // C layout (row lg + 4q, col lr)
+            return reinterpret_cast<double*>(reinterpret_cast<char*>(base) + oc) + 4 * q * PT;
+        };
+        auto apos = [&](const double* base, int c) -> const double* {   // A/B operand (row lr, k 4c + lg)
+            return reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + oa) + 4 * c;
+        };
+        // (A)
+#pragma unroll
+        for (int s = 0; s < PR_SLOTS; ++s)
+            if (ti[s] == j && tk[s] == j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) *cpos(Dt, q) = acc[s][q];
+            }
+        __syncthreads();
+        PSTAMP(2 + 4 * j);
+        // (B)
+        if (wave == 0) {
+            const int bad = diag_factor16(Dt, Di, ivs, Dinv + size_t(j) * 256, lane, n - 16 * j);
+            if (lane == 0 && bad && fail == 0) fail = 16 * j + bad;
+        }
+        __syncthreads();
+        PSTAMP(3 + 4 * j);
+        // (C)
+#pragma unroll
+        for (int s = 0; s < PR_SLOTS; ++s) {
+            if (tk[s] != j) continue;
+            if (ti[s] == j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[s][q] = *cpos(Dt, q);
+                continue;
+            }
+            double* Pi = P + ti[s] * PTILE;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *cpos(Pi, q) = acc[s][q];
+            wave_lds_sync();
+            d4 rr = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) rr = __builtin_amdgcn_mfma_f64_16x16x4f64(*apos(Pi, c), *apos(Di, c), rr, 0, 0, 0);
+            wave_lds_sync();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *cpos(Pi, q) = rr[q];
+            acc[s] = rr;
+        }
+        __syncthreads();
+        PSTAMP(4 + 4 * j);
+        // (D)
+#pragma unroll
+        for (int s = 0; s < PR_SLOTS; ++s) {
+            if (tk[s] <= j) continue;
+            const double* Pa = P + ti[s] * PTILE;
+            const double* Pb = P + tk[s] * PTILE;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-*apos(Pa, c), *apos(Pb, c), acc[s], 0, 0, 0);
+        }
     }
     __syncthreads();
-    // 2x2 tile: rows r0, r0+16 ; vectors c0, c0+16
-    const int r0 = tid >> 4;        // 0..15
-    const int c0 = tid & 15;        // 0..15
-    for (int i0 = 0; i0 < n; i0 += NB) {
-        const int ib = min(NB, n - i0);
-        {
-            const int ra = min(i0 + r0, n - 1), rb = min(i0 + r0 + 16, n - 1);
-            double t00 = Xs[ra * S + c0], t01 = Xs[ra * S + c0 + 16];
-            double t10 = Xs[rb * S + c0], t11 = Xs[rb * S + c0 + 16];
-            const double* la = L + size_t(ra) * n;
-            const double* lb = L + size_t(rb) * n;
-            for (int j = 0; j < i0; ++j) {
-                const double a = la[j], b = lb[j];
-                const double x0 = Xs[j * S + c0], x1 = Xs[j * S + c0 + 16];
-                t00 -= a * x0; t01 -= a * x1;
-                t10 -= b * x0; t11 -= b * x1;
+    PSTAMP(1);
+    // store L (lower) and zero the mirrored upper tiles (opaque lane indices: stops the compiler from
+    // keeping every tile's global addresses live from the initial load)
+    int sg = lg, sr = lr;
+    asm volatile("" : "+v"(sg), "+v"(sr));
+#pragma unroll
+    for (int s = 0; s < PR_SLOTS; ++s) {
+        if (ti[s] < 0) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 16 * ti[s] + sg + 4 * q, col = 16 * tk[s] + sr;
+            if (row < n && col < n) {
+                G[size_t(row) * n + col] = (col <= row) ? acc[s][q] : 0.0;
+                if (ti[s] != tk[s]) G[size_t(col) * n + row] = 0.0;
             }
-            Ts[r0][c0] = t00; Ts[r0][c0 + 16] = t01;
-            Ts[r0 + 16][c0] = t10; Ts[r0 + 16][c0 + 16] = t11;
         }
-        __syncthreads();
-        {
-            double x00 = 0, x01 = 0, x10 = 0, x11 = 0;
-            const double* da = Dinv + size_t(min(i0 + r0, n - 1)) * NB;
-            const double* db = Dinv + size_t(min(i0 + r0 + 16, n - 1)) * NB;
-            for (int k = 0; k < NB; ++k) {
-                const double a = da[k], b = db[k];
-                const double t0 = Ts[k][c0], t1 = Ts[k][c0 + 16];
-                x00 += a * t0; x01 += a * t1;
-                x10 += b * t0; x11 += b * t1;
-            }
-            if (r0 < ib) { Xs[(i0 + r0) * S + c0] = x00; Xs[(i0 + r0) * S + c0 + 16] = x01; }
-            if (r0 + 16 < ib) { Xs[(i0 + r0 + 16) * S + c0] = x10; Xs[(i0 + r0 + 16) * S + c0 + 16] = x11; }
-        }
-        __syncthreads();
     }
-    for (int e = tid; e < n * NB; e += 256) {
+    __syncthreads();
+    if (tid == 0) status[0] = fail;
+}
+
+__global__ void __launch_bounds__(PR_THREADS) k_potrf_rr(double* __restrict__ G, int n, double shift_rel,
+                                                         double* __restrict__ Dinv, int* __restrict__ status,
+                                                         double* __restrict__ info) {
+    potrf_rr_body(G, n, shift_rel, Dinv, status, info);
+}
+
+// Independent factorisations, one workgroup each (e.g. the left Gram matrices of every TT edge).
+__global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b, double shift_rel) {
+    const int i = blockIdx.x;
+    potrf_rr_body(b.G[i], b.n[i], shift_rel, b.Dinv[i], b.status + i, nullptr);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Triangular solve X = L^{-1} Y, 16 right-hand sides per workgroup of 4 waves, fp64 MFMA.
+// Block-row I: T_I = Y_I - sum_{J<I} L_IJ X_J with the J-sum split over the waves (J = wave mod 4;
+// the wave keeps its X_J tiles in registers in the MFMA C layout, which is exactly the B-operand
+// layout of the next products), partials reduced through LDS, then every wave forms
+// X_I = Dinv_I T_I redundantly (no second barrier). L_IJ and Dinv_I are read from L2 one block-row
+// ahead (register prefetch). Dinv: 16x16 diagonal-block inverses; dld = 16 (k_potrf_rr layout,
+// block J at Dinv + 256 J) or 32 (k_potrf layout: the 16x16 diagonal sub-blocks of the 32x32 block
+// inverses are the 16-block inverses).
+template <bool COLS, int TMAX>
+__global__ void __launch_bounds__(256) k_trsm16(const double* __restrict__ L, const double* __restrict__ Dinv, int dld,
+                                                int n, const double* __restrict__ Y, size_t ldy, double* __restrict__ X,
+                                                size_t ldx, int nvec) {
+    constexpr int JS = TMAX / 4;
+    __shared__ double Xs[TMAX * 16 * PT];
+    __shared__ double red[2][4][256];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lg = lane >> 4;
+    const int v0 = blockIdx.x * 16;
+    const int T = (n + 15) >> 4;
+    const int np = T * 16;
+    for (int e = tid; e < np * 16; e += 256) {
         int i, v;
-        if (COLS) { i = e / NB; v = e % NB; } else { v = e / n; i = e % n; }
-        if (v < nv) {
-            if (COLS) X[size_t(i) * ldx + v0 + v] = Xs[i * S + v];
-            else X[size_t(v0 + v) * ldx + i] = Xs[i * S + v];
+        if (COLS) { i = e >> 4; v = e & 15; } else { v = e / np; i = e - v * np; }
+        double y = 0.0;
+        if (i < n && v0 + v < nvec) y = COLS ? Y[size_t(i) * ldy + v0 + v] : Y[size_t(v0 + v) * ldy + i];
+        Xs[i * PT + v] = y;
+    }
+    auto dinv_at = [&](int I, int c) -> double {
+        const int off = (dld == 32) ? 16 * (I & 1) : 0;
+        return Dinv[size_t(16 * I + lr) * dld + off + 4 * c + lg];
+    };
+    d4 xr[JS];
+    double la[JS][4], lb[JS][4], da[4], db[4];
+#pragma unroll
+    for (int js = 0; js < JS; ++js) {
+        xr[js] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) la[js][c] = 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) da[c] = dinv_at(0, c);
+    __syncthreads();
+    for (int I = 0; I < T; ++I) {
+        if (I + 1 < T) {   // prefetch block-row I+1
+            const int row = 16 * (I + 1) + lr;
+#pragma unroll
+            for (int js = 0; js < JS; ++js) {
+                const int J = wave + 4 * js;
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    lb[js][c] = (J <= I && row < n) ? L[size_t(row) * n + 16 * J + 4 * c + lg] : 0.0;
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) db[c] = dinv_at(I + 1, c);
+        }
+        d4 y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = Xs[(16 * I + lg + 4 * q) * PT + lr];
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int js = 0; js < JS; ++js) {
+            if (wave + 4 * js >= I) continue;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(la[js][c], xr[js][c], acc, 0, 0, 0);
+        }
+        double* rb = red[I & 1][0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rb[wave * 256 + q * 64 + lane] = acc[q];
+        __syncthreads();
+        d4 t;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            t[q] = y[q] - ((rb[q * 64 + lane] + rb[256 + q * 64 + lane]) + (rb[512 + q * 64 + lane] + rb[768 + q * 64 + lane]));
+        d4 x = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) x = __builtin_amdgcn_mfma_f64_16x16x4f64(da[c], t[c], x, 0, 0, 0);
+        if ((I & 3) == wave) {
+#pragma unroll
+            for (int js = 0; js < JS; ++js)
+                if (js == (I >> 2)) xr[js] = x;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) Xs[(16 * I + lg + 4 * q) * PT + lr] = x[q];
+        }
+#pragma unroll
+        for (int js = 0; js < JS; ++js)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) la[js][c] = lb[js][c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) da[c] = db[c];
+    }
+    __syncthreads();
+    for (int e = tid; e < np * 16; e += 256) {
+        int i, v;
+        if (COLS) { i = e >> 4; v = e & 15; } else { v = e / np; i = e - v * np; }
+        if (i < n && v0 + v < nvec) {
+            if (COLS) X[size_t(i) * ldx + v0 + v] = Xs[i * PT + v];
+            else X[size_t(v0 + v) * ldx + i] = Xs[i * PT + v];
         }
     }
 }
@@ -578,11 +884,30 @@ __global__ void __launch_bounds__(1024) k_svd_finish(const double* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------------ launchers
+// Dinv row stride: k_potrf_rr (n <= 256) writes 16x16 blocks, k_potrf 32x32 blocks.
+static int dinv_ld(int n) { return n <= PR_TMAX * 16 ? 16 : 32; }
+
 void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int* status_dev, double* info_dev) {
     XRS_REQUIRE(n >= 1 && n <= PMAX, "potrf: n out of range for the single-workgroup kernel");
     KernelTimer timer(h, XRS_KFAM_QR, double(n) * n * n / 3.0, 16.0 * double(n) * n);
-    hipLaunchKernelGGL(k_potrf, dim3(1), dim3(POT_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
-    check_launch("k_potrf");
+    if (dinv_ld(n) == 16) {
+        hipLaunchKernelGGL(k_potrf_rr, dim3(1), dim3(PR_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
+        check_launch("k_potrf_rr");
+    } else {
+        hipLaunchKernelGGL(k_potrf, dim3(1), dim3(POT_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
+        check_launch("k_potrf");
+    }
+}
+
+void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count, double shift_rel) {
+    XRS_REQUIRE(count >= 0 && count <= kPotrfBatchMax, "potrf_batched: batch too large");
+    if (count == 0) return;
+    for (int i = 0; i < count; ++i) XRS_REQUIRE(b.n[i] >= 1 && b.n[i] <= PR_TMAX * 16, "potrf_batched: n out of range");
+    double fl = 0.0;
+    for (int i = 0; i < count; ++i) fl += double(b.n[i]) * b.n[i] * b.n[i] / 3.0;
+    KernelTimer timer(h, XRS_KFAM_QR, fl, 0.0);
+    hipLaunchKernelGGL(k_potrf_rr_batched, dim3(count), dim3(PR_THREADS), 0, h->stream, b, shift_rel);
+    check_launch("k_potrf_rr_batched");
 }
 
 void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n, const double* Y, size_t ldy, double* X,
@@ -590,19 +915,17 @@ void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n,
     if (nvec <= 0) return;
     XRS_REQUIRE(n >= 1 && n <= PMAX, "trsm: n out of range");
     KernelTimer timer(h, XRS_KFAM_QR, double(n) * n * nvec, 8.0 * (2.0 * double(n) * nvec + double(n) * n));
-    const size_t lds = size_t(n) * (NB + 1) * sizeof(double);
-    static bool attr_set = false;
-    if (!attr_set) {
-        XRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm<false>), hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024));
-        XRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_trsm<true>), hipFuncAttributeMaxDynamicSharedMemorySize, 136 * 1024));
-        attr_set = true;
+    const unsigned blocks = unsigned((nvec + 15) / 16);
+    const int dld = dinv_ld(n);
+#define XRS_TRSM(C_, T_) \
+    hipLaunchKernelGGL((k_trsm16<C_, T_>), dim3(blocks), dim3(256), 0, h->stream, L, Dinv, dld, n, Y, ldy, X, ldx, nvec)
+    if (n <= 256) {
+        if (cols) XRS_TRSM(true, 16); else XRS_TRSM(false, 16);
+    } else {
+        if (cols) XRS_TRSM(true, 32); else XRS_TRSM(false, 32);
     }
-    const unsigned blocks = unsigned((nvec + NB - 1) / NB);
-    if (cols)
-        hipLaunchKernelGGL(k_trsm<true>, dim3(blocks), dim3(256), lds, h->stream, L, Dinv, n, Y, ldy, X, ldx, nvec);
-    else
-        hipLaunchKernelGGL(k_trsm<false>, dim3(blocks), dim3(256), lds, h->stream, L, Dinv, n, Y, ldy, X, ldx, nvec);
-    check_launch("k_trsm");
+#undef XRS_TRSM
+    check_launch("k_trsm16");
 }
 
 size_t qrcp(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C, bool pivot, bool abs_r00,

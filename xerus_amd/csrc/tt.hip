@@ -204,8 +204,99 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
     t.r[k] = kk;
 }
 
+// ---- certified fast path of round() ------------------------------------------------------------
+// round() can only change the tensor through a cut: a QC rank drop in the left-to-right sweep
+// (|R_kk| < 16 eps R_00, blasLapackWrapper.cpp:268-272) or an SVD cut in round_edge (sigma_j <= eps
+// sigma_0 or j >= maxRank, tensor.cpp:1462-1474). When the ranks are within maxRanks and every edge
+// unfolding U_k = X_{<k} X_{>=k} is provably well conditioned, neither can happen, and the result is
+// the input tensor in right-canonical form (core at 0) with the same ranks -- what one right-to-left
+// orthogonalisation sweep produces. Proof obligations:
+//   kappa(X_{<k}) <= 1/c_X: Gram G_k = X_{<k}^T X_{<k} built by the left chain G_{k+1} = M^T (G_k M)
+//   from the ORIGINAL cores, then a Cholesky of G_k - tau tr(G_k) I succeeding for every k (one batched
+//   launch) gives lambda_min(G_k) >= (tau - rounding) tr(G_k) >= tau/4 tr(G_k), c_X = sqrt(tau)/2;
+//   kappa(L_k) <= 1/c_L from the certified LQ of core k (orthogonalize);
+//   then sigma_min(U)/sigma_max(U) >= c_X c_L > eps (>= 16 eps needed for the QC rule too, since
+//   |R_kk| >= sigma_min for any triangular factor).
+// Any failed obligation falls back to the reference's two-sweep algorithm, from the failing edge on.
+constexpr double kLeftShift = 1e-9;
+
+bool left_grams_certified(TT& t) {
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    for (size_t k = 1; k < d; ++k)
+        if (t.r[k] > 256) return false;   // batched single-workgroup Cholesky limit
+    std::vector<DevBuf> G;
+    G.reserve(d);
+    size_t tmax = 1;
+    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.r[k] * t.cols_right(k));
+    DevBuf T(h, tmax * 8);
+    G.emplace_back(h, t.r[1] * t.r[1] * 8);
+    gemm(h, G[0].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
+    for (size_t k = 1; k + 1 < d; ++k) {
+        const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
+        gemm(h, T.d(), a, cols, 1.0, G[k - 1].d(), a, false, a, t.core[k], cols, false);         // G_k M
+        G.emplace_back(h, b * b * 8);
+        gemm(h, G[k].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T.d(), b, false);          // M^T (G_k M)
+    }
+    const int cnt = int(d - 1);
+    DevBuf Dv(h, size_t(cnt) * 256 * 17 * 8), st(h, size_t(cnt) * 4 + 64);
+    int* hs = static_cast<int*>(h->host_scratch);
+    for (int b0 = 0; b0 < cnt; b0 += kPotrfBatchMax) {
+        PotrfBatch pb{};
+        const int c = std::min(kPotrfBatchMax, cnt - b0);
+        for (int i = 0; i < c; ++i) {
+            pb.G[i] = G[b0 + i].d();
+            pb.n[i] = int(t.r[b0 + i + 1]);
+            pb.Dinv[i] = Dv.d() + size_t(b0 + i) * 256 * 17;
+        }
+        pb.status = st.as<int>() + b0;
+        potrf_batched(h, pb, c, -kLeftShift);
+    }
+    XRS_HIP(hipMemcpyAsync(hs, st.d(), size_t(cnt) * 4, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    for (int i = 0; i < cnt; ++i)
+        if (hs[i] != 0) return false;
+    return true;
+}
+
+void truncate_edge(TT& t, size_t k, size_t max_rank, double eps);
+void orth_right(TT& t, size_t k);
+
+bool round_fast(TT& t, const size_t* max_ranks, double eps) {
+    const size_t d = t.d;
+    if (d < 2 || exceeds_maximal_ranks(t)) return false;
+    for (size_t k = 1; k < d; ++k)
+        if (t.r[k] > max_ranks[k - 1] || t.r[k] > t.cols_right(k) || t.r[k] > 256) return false;
+    const double cX = 0.5 * std::sqrt(kLeftShift);
+    if (!(eps < 0.5 * cX * 1e-5)) return false;   // LQ certificates are ~1e-6; larger eps: reference path
+    if (!left_grams_certified(t)) return false;
+    for (size_t k = d - 1; k >= 1; --k) {
+        const size_t m = t.r[k], nn = t.cols_right(k), prow = t.rows_left(k - 1);
+        double* Q = t.alloc(m * nn);
+        double* L = t.alloc(m * m);
+        const OrthResult o = orthogonalize(t.h, t.core[k], m, nn, true, Q, L);
+        const double c = o.certified ? cX * o.cert_ratio : 0.0;
+        if (!(c > 16.0 * 2.220446049250313e-16 && eps < 0.5 * c)) {
+            // certificate failed at edge k: edges > k are done exactly (no cut possible there); finish
+            // with the reference algorithm: left-orthogonalise cores 0..k-1 (core k absorbs), truncate.
+            t.release(Q);
+            t.release(L);
+            for (size_t j = 0; j < k; ++j) orth_right(t, j);
+            for (size_t kk = k; kk >= 1; --kk) truncate_edge(t, kk, max_ranks[kk - 1], eps);
+            return true;
+        }
+        double* prv = t.alloc(prow * m);
+        gemm(t.h, prv, prow, m, 1.0, t.core[k - 1], m, false, m, L, m, false);
+        t.release(L);
+        t.replace(k, Q);
+        t.replace(k - 1, prv);
+    }
+    return true;
+}
+
 void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
+    if (round_fast(t, max_ranks, eps)) return;
     // canonicalize_right (ttNetwork.cpp:638-640, 654)
     const size_t start = canonicalized ? core_pos : 0;
     for (size_t k = start; k + 1 < d; ++k) orth_right(t, k);
