@@ -262,68 +262,118 @@ __device__ __forceinline__ double row_bcast_d(double v) {
     return u.d;
 }
 
+// One elimination step of the 16x16 diagonal block, LDL^T form so that the pivot dependency chain is
+// only bcast -> rcp (+2 Newton) -> multiplier -> next pivot update. Lane r of every 16-lane row keeps
+// row r of the symmetric Schur complement (a[l], all 16 columns, redundantly per row group) and 4
+// columns (g + 4t, g = row group) of W = unit-L^{-1}, built by applying the same row operations to I.
 template <int K>
-__device__ __forceinline__ void factor_step(double (&a)[16], double* ivs, int lane, int valid, int& bad) {
-    double dkk = row_bcast_d<K>(a[K]);
-    const bool ok = (dkk > 0.0) && (dkk < 1.0e300);   // rejects <= 0, NaN and Inf
-    if (!ok && bad == 0 && K < valid) bad = K + 1;
-    if (!ok) dkk = 1.0;
-    const double v = rsqrt_nr(dkk);
-    if (lane == 0) ivs[K] = v;
-    const double lrk = a[K] * v;                       // L_rk (r > k); sqrt(dkk) for r == k
-    const double nl = -lrk * v;
+__device__ __forceinline__ void factor_step(double (&a)[16], double (&w)[4], double* dsh, int lane, int valid, int& bad) {
+    const double dkk = row_bcast_d<K>(a[K]);
+    if (!((dkk > 0.0) && (dkk < 1.0e300)) && bad == 0 && K < valid) bad = K + 1;   // off the chain
+    if (lane == 0) dsh[K] = dkk;
+    double r = __builtin_amdgcn_rcp(dkk);
+    r = fma(r, fma(-dkk, r, 1.0), r);
+    r = fma(r, fma(-dkk, r, 1.0), r);
+    const double m = a[K] * r;                              // S_rK / S_KK
 #pragma unroll
-    for (int l = K + 1; l < 16; ++l) a[l] = fma(nl, row_bcast_d<K>(a[l]), a[l]);
-    a[K] = lrk;
+    for (int l = K + 1; l < 16; ++l) a[l] = fma(-m, row_bcast_d<K>(a[l]), a[l]);
+    const double mm = ((lane & 15) > K) ? m : 0.0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) w[t] = fma(-mm, row_bcast_d<K>(w[t]), w[t]);
 }
 
 template <int K>
-__device__ __forceinline__ void factor_all(double (&a)[16], double* ivs, int lane, int valid, int& bad) {
+__device__ __forceinline__ void factor_all(double (&a)[16], double (&w)[4], double* dsh, int lane, int valid, int& bad) {
     if constexpr (K < 16) {
-        factor_step<K>(a, ivs, lane, valid, bad);
-        factor_all<K + 1>(a, ivs, lane, valid, bad);
+        factor_step<K>(a, w, dsh, lane, valid, bad);
+        factor_all<K + 1>(a, w, dsh, lane, valid, bad);
     }
 }
 
 // (B): factor the 16x16 tile in Dt (full symmetric), leave L_jj (lower, zero upper) in Dt and
 // L_jj^{-1} in Di and dinv_out (row-major 16x16). Returns 1 + first failing local column or 0.
-// Every 16-lane row of wave 0 factors the tile redundantly (lane r & 15 owns row r of the Schur
-// complement; column k of L is lane k's row, broadcast with DPP row_newbcast).
-__device__ __forceinline__ int diag_factor16(double* Dt, double* Di, double* ivs, double* __restrict__ dinv_out,
+// With d_c the pivots and a[c] the eliminated column values: L_rc = a[c] / sqrt(d_c) (c <= r) and
+// L^{-1}_rc = W_rc / sqrt(d_r).
+__device__ __forceinline__ int diag_factor16(double* Dt, double* Di, double* dsh, double* __restrict__ dinv_out,
                                              int lane, int valid) {
-    const int r = lane & 15;
-    double a[16];
+    const int r = lane & 15, g = lane >> 4;
+    double a[16], w[4];
 #pragma unroll
     for (int c = 0; c < 16; ++c) a[c] = Dt[r * PT + c];
-    int bad = 0;
-    factor_all<0>(a, ivs, lane, valid, bad);
-    if (lane < 16) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c) Dt[r * PT + c] = (c <= r) ? a[c] : 0.0;
-    }
+    for (int t = 0; t < 4; ++t) w[t] = (g + 4 * t == r) ? 1.0 : 0.0;
+    int bad = 0;
+    factor_all<0>(a, w, dsh, lane, valid, bad);
     wave_lds_sync();
 #ifdef XRS_POTRF_STAMPS
     if (lane == 0) g_potrf_stamps[1000 + blockIdx.x] = __builtin_amdgcn_s_memtime();
 #endif
-    // column c of L^{-1}, right-looking (dependency chain of 2 ops per k): x_k *= 1/L_kk, x_i -= L_ik x_k
-    const int c = lane & 15;
-    double x[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = (i == c) ? 1.0 : 0.0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        x[k] *= ivs[k];
-#pragma unroll
-        for (int i = k + 1; i < 16; ++i) x[i] = fma(-Dt[i * PT + k], x[k], x[i]);
-    }
     if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            Di[i * PT + c] = x[i];
-            dinv_out[i * 16 + c] = x[i];
-        }
+        for (int c = 0; c < 16; ++c) Dt[r * PT + c] = (c <= r) ? a[c] : 0.0;   // unscaled, rescaled below
     }
+    const double rsr = rsqrt_nr(dsh[r]);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const double v = w[t] * rsr;
+        Di[r * PT + g + 4 * t] = v;
+        dinv_out[r * 16 + g + 4 * t] = v;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {   // element (row, col) = (lane >> 2, 4 (lane & 3) + e)
+        const int rr = lane >> 2, cc = 4 * (lane & 3) + e;
+        if (cc <= rr) Dt[rr * PT + cc] *= rsqrt_nr(dsh[cc]);
+    }
+    wave_lds_sync();
     return bad;
+}
+
+// (D) for a pair of slots (P, P-1): tiles (i,k) with k > j get G_ik -= L_ij L_kj^T. Slots are ordered by
+// column, so the active ones are a suffix; the pair's operands are loaded together and the two MFMA
+// chains interleaved (slot P-1 inactive -> zero operands, exact no-op on its accumulator).
+template <int P>
+__device__ __forceinline__ void trail_pair(d4 (&acc)[PR_SLOTS], const int (&ti)[PR_SLOTS], const int (&tk)[PR_SLOTS], int j,
+                                           const double* Pbuf, int oa) {
+    // slot P may be a padding slot (tk = -1) above an active slot P-1: test both
+    const bool hi = tk[P] > j;
+    bool lo = false;
+    if constexpr (P > 0) lo = tk[P - 1] > j;
+    if (!hi && !lo) return;
+    auto op = [&](int tile, int c) -> double {
+        return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(Pbuf + max(tile, 0) * PTILE) + oa + 32 * c);
+    };
+    double a1[4], b1[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        a1[c] = hi ? -op(ti[P], c) : 0.0;
+        b1[c] = hi ? op(tk[P], c) : 0.0;
+    }
+    if constexpr (P > 0) {
+        double a0[4], b0[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = lo ? -op(ti[P - 1], c) : 0.0;
+            b0[c] = lo ? op(tk[P - 1], c) : 0.0;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            acc[P] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[c], b1[c], acc[P], 0, 0, 0);
+            acc[P - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[c], b0[c], acc[P - 1], 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[P] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[c], b1[c], acc[P], 0, 0, 0);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void trail_all(d4 (&acc)[PR_SLOTS], const int (&ti)[PR_SLOTS], const int (&tk)[PR_SLOTS], int j,
+                                          const double* Pbuf, int oa) {
+    if constexpr (P >= 0) {
+        trail_pair<P>(acc, ti, tk, j, Pbuf, oa);
+        trail_all<P - 2>(acc, ti, tk, j, Pbuf, oa);
+    }
 }
 
 __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
@@ -437,15 +487,7 @@ __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, dou
         __syncthreads();
         PSTAMP(4 + 4 * j);
         // (D)
-#pragma unroll
-        for (int s = 0; s < PR_SLOTS; ++s) {
-            if (tk[s] <= j) continue;
-            const double* Pa = P + ti[s] * PTILE;
-            const double* Pb = P + tk[s] * PTILE;
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-                acc[s] = __builtin_amdgcn_mfma_f64_16x16x4f64(-*apos(Pa, c), *apos(Pb, c), acc[s], 0, 0, 0);
-        }
+        trail_all<PR_SLOTS - 1>(acc, ti, tk, j, P, oa);
     }
     __syncthreads();
     PSTAMP(1);
@@ -476,9 +518,9 @@ __global__ void __launch_bounds__(PR_THREADS) k_potrf_rr(double* __restrict__ G,
 }
 
 // Independent factorisations, one workgroup each (e.g. the left Gram matrices of every TT edge).
-__global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b, double shift_rel) {
+__global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
     const int i = blockIdx.x;
-    potrf_rr_body(b.G[i], b.n[i], shift_rel, b.Dinv[i], b.status + i, nullptr);
+    potrf_rr_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -899,14 +941,14 @@ void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int
     }
 }
 
-void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count, double shift_rel) {
+void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count) {
     XRS_REQUIRE(count >= 0 && count <= kPotrfBatchMax, "potrf_batched: batch too large");
     if (count == 0) return;
     for (int i = 0; i < count; ++i) XRS_REQUIRE(b.n[i] >= 1 && b.n[i] <= PR_TMAX * 16, "potrf_batched: n out of range");
     double fl = 0.0;
     for (int i = 0; i < count; ++i) fl += double(b.n[i]) * b.n[i] * b.n[i] / 3.0;
     KernelTimer timer(h, XRS_KFAM_QR, fl, 0.0);
-    hipLaunchKernelGGL(k_potrf_rr_batched, dim3(count), dim3(PR_THREADS), 0, h->stream, b, shift_rel);
+    hipLaunchKernelGGL(k_potrf_rr_batched, dim3(count), dim3(PR_THREADS), 0, h->stream, b);
     check_launch("k_potrf_rr_batched");
 }
 

@@ -10,16 +10,17 @@ constexpr int kSmallMax = 512;  // largest n handled by the single-workgroup ker
 // diagonal blocks. *status_dev = 0 on success, else 1 + first failing column; info_dev[0] = trace(G)
 // (may be null). Enqueued only.
 void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int* status_dev, double* info_dev = nullptr);
-// Batch of independent Cholesky factorisations (n <= 256 each), one workgroup per matrix; status[i] as
-// for potrf. Dinv[i] needs n_i * 16 doubles (rounded up to a multiple of 16 rows).
-constexpr int kPotrfBatchMax = 32;
+// Batch of independent Cholesky factorisations (n <= 256 each), one workgroup per matrix, each with its
+// own relative diagonal shift; status[i] as for potrf. Dinv[i] needs ceil(n_i/16)*256 doubles.
+constexpr int kPotrfBatchMax = 48;
 struct PotrfBatch {
     double* G[kPotrfBatchMax];
     double* Dinv[kPotrfBatchMax];
+    double shift[kPotrfBatchMax];
     int n[kPotrfBatchMax];
     int* status;
 };
-void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count, double shift_rel);
+void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count);
 // X = L^{-1} Y. cols=false: the RHS vectors are the nvec rows of Y (ld ldy); cols=true: the nvec columns.
 void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n, const double* Y, size_t ldy, double* X,
           size_t ldx, int nvec);

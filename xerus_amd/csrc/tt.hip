@@ -218,72 +218,189 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
 //   then sigma_min(U)/sigma_max(U) >= c_X c_L > eps (>= 16 eps needed for the QC rule too, since
 //   |R_kk| >= sigma_min for any triangular factor).
 // Any failed obligation falls back to the reference's two-sweep algorithm, from the failing edge on.
-constexpr double kLeftShift = 1e-9;
+constexpr double kGramShift = 1e-9;
 
-bool left_grams_certified(TT& t) {
+// Gram chains from the current cores (k = 1..d-1, index k):
+//   left  G_k = X_{<k}^T X_{<k}:  G_1 = M_0^T M_0, G_{k+1} = M_k^T (G_k M_k)   (M_k: r_k x n_k r_{k+1})
+//   right H_k = X_{>=k} X_{>=k}^T: H_{d-1} = M M^T, H_k = M_k (I (x) H_{k+1}) M_k^T
+void left_grams(TT& t, std::vector<DevBuf>& G) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
-    for (size_t k = 1; k < d; ++k)
-        if (t.r[k] > 256) return false;   // batched single-workgroup Cholesky limit
-    std::vector<DevBuf> G;
-    G.reserve(d);
+    G.clear();
+    G.resize(d);
     size_t tmax = 1;
-    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.r[k] * t.cols_right(k));
+    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
     DevBuf T(h, tmax * 8);
-    G.emplace_back(h, t.r[1] * t.r[1] * 8);
-    gemm(h, G[0].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
+    G[1] = DevBuf(h, t.r[1] * t.r[1] * 8);
+    gemm(h, G[1].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
     for (size_t k = 1; k + 1 < d; ++k) {
         const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-        gemm(h, T.d(), a, cols, 1.0, G[k - 1].d(), a, false, a, t.core[k], cols, false);         // G_k M
-        G.emplace_back(h, b * b * 8);
-        gemm(h, G[k].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T.d(), b, false);          // M^T (G_k M)
+        gemm(h, T.d(), a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
+        G[k + 1] = DevBuf(h, b * b * 8);
+        gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T.d(), b, false);
     }
-    const int cnt = int(d - 1);
-    DevBuf Dv(h, size_t(cnt) * 256 * 17 * 8), st(h, size_t(cnt) * 4 + 64);
-    int* hs = static_cast<int*>(h->host_scratch);
+}
+
+void right_grams(TT& t, std::vector<DevBuf>& H) {
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    H.clear();
+    H.resize(d);
+    size_t tmax = 1;
+    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
+    DevBuf T(h, tmax * 8);
+    const size_t last = d - 1, rl = t.r[last], cl = t.cols_right(last);
+    H[last] = DevBuf(h, rl * rl * 8);
+    gemm(h, H[last].d(), rl, rl, 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
+    for (size_t k = last - 1; k >= 1; --k) {
+        const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
+        gemm(h, T.d(), a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
+        H[k] = DevBuf(h, a * a * 8);
+        gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T.d(), cols, true);         // M_k T^T
+    }
+}
+
+struct DevIdArgs {
+    const double* G[64];
+    int n[64];
+    double* out;
+};
+
+// max |G_i - I| of a batch of square matrices, one workgroup each
+__global__ void __launch_bounds__(256) k_dev_identity_many(const DevIdArgs args) {
+    const double* G = args.G[blockIdx.x];
+    const int n = args.n[blockIdx.x];
+    __shared__ double red[4];
+    double mx = 0.0;
+    for (int e = threadIdx.x; e < n * n; e += 256) {
+        const double v = fabs(G[e] - ((e / n) == (e % n) ? 1.0 : 0.0));
+        mx = (v > mx || v != v) ? v : mx;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double q = __shfl_xor(mx, o, 64);
+        mx = (q > mx || q != q) ? q : mx;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double m = red[0];
+        for (int i = 1; i < 4; ++i) m = (red[i] > m || red[i] != red[i]) ? red[i] : m;
+        args.out[blockIdx.x] = m;
+    }
+}
+
+void rl_sweep(TT& t, const size_t* max_ranks, double eps, double cX, size_t from);
+
+// Chain form of the certified round: both Gram chains, ONE batched launch of 3(d-1) Cholesky
+// factorisations (left/right Grams shifted down by tau tr: certificates kappa(X_{<k}), kappa(X_{>=k})
+// <= 2/sqrt(tau); right Grams unshifted: H_k = L_k L_k^T), then every core is transformed
+// independently, C_k = L_k^{-1} M_k (I (x) L_{k+1}) (right-orthonormal rows in exact arithmetic),
+// C_0 = M_0 (I (x) L_1). No factorisation sits on a sequential chain; the per-core Gram check
+// max|C_k C_k^T - I| <= 1e-13 confirms the orthogonality, else the sequential CholeskyQR2 sweep
+// re-orthogonalises the (same-tensor) cores.
+bool round_chain(TT& t, const size_t* max_ranks, double eps) {
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    if (d < 2 || d > 65 || exceeds_maximal_ranks(t)) return false;
+    for (size_t k = 1; k < d; ++k)
+        if (t.r[k] > max_ranks[k - 1] || t.r[k] > 256) return false;
+    const double cX = 0.5 * std::sqrt(kGramShift);
+    if (!(eps < 0.25 * cX * cX)) return false;
+    std::vector<DevBuf> G, H, Hs;
+    left_grams(t, G);
+    right_grams(t, H);
+    Hs.resize(d);
+    const int cnt = int(3 * (d - 1));
+    DevBuf Dv(h, (d - 1) * 256 * 16 * 8 + 8), Dscr(h, 2 * (d - 1) * 256 * 16 * 8 + 8), st(h, size_t(cnt) * 4 + 64);
+    std::vector<double*> dinv(d, nullptr);
+    struct Job { double* G; double* Dinv; double shift; int n; };
+    std::vector<Job> jobs;
+    for (size_t k = 1; k < d; ++k) {
+        const size_t a = t.r[k];
+        Hs[k] = DevBuf(h, a * a * 8);
+        XRS_HIP(hipMemcpyAsync(Hs[k].d(), H[k].d(), a * a * 8, hipMemcpyDeviceToDevice, h->stream));
+        dinv[k] = Dv.d() + (k - 1) * 256 * 16;
+        jobs.push_back({H[k].d(), dinv[k], 0.0, int(a)});
+        jobs.push_back({G[k].d(), Dscr.d() + (2 * (k - 1)) * 256 * 16, -kGramShift, int(a)});
+        jobs.push_back({Hs[k].d(), Dscr.d() + (2 * (k - 1) + 1) * 256 * 16, -kGramShift, int(a)});
+    }
     for (int b0 = 0; b0 < cnt; b0 += kPotrfBatchMax) {
         PotrfBatch pb{};
         const int c = std::min(kPotrfBatchMax, cnt - b0);
         for (int i = 0; i < c; ++i) {
-            pb.G[i] = G[b0 + i].d();
-            pb.n[i] = int(t.r[b0 + i + 1]);
-            pb.Dinv[i] = Dv.d() + size_t(b0 + i) * 256 * 17;
+            pb.G[i] = jobs[b0 + i].G;
+            pb.Dinv[i] = jobs[b0 + i].Dinv;
+            pb.shift[i] = jobs[b0 + i].shift;
+            pb.n[i] = jobs[b0 + i].n;
         }
         pb.status = st.as<int>() + b0;
-        potrf_batched(h, pb, c, -kLeftShift);
+        potrf_batched(h, pb, c);
     }
+    int* hs = static_cast<int*>(h->host_scratch);
     XRS_HIP(hipMemcpyAsync(hs, st.d(), size_t(cnt) * 4, hipMemcpyDeviceToHost, h->stream));
     XRS_HIP(hipStreamSynchronize(h->stream));
     for (int i = 0; i < cnt; ++i)
         if (hs[i] != 0) return false;
+    // independent per-core transforms
+    std::vector<double*> C(d, nullptr);
+    size_t wmax = 1;
+    for (size_t k = 0; k < d; ++k) wmax = std::max(wmax, t.size(k));
+    DevBuf W(h, wmax * 8);
+    for (size_t k = 0; k < d; ++k) {
+        const size_t a = t.r[k], b = t.r[k + 1], rows = t.rows_left(k), cols = t.cols_right(k);
+        C[k] = t.alloc(t.size(k));
+        const double* src = t.core[k];
+        if (k + 1 < d) {   // M_k (I (x) L_{k+1}): (r_k n_k) x r_{k+1} times r_{k+1} x r_{k+1}
+            gemm(h, k == 0 ? C[k] : W.d(), rows, b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);
+            src = W.d();
+        }
+        if (k > 0) trsm(h, true, H[k].d(), dinv[k], int(a), src, cols, C[k], cols, int(cols));
+        else if (k + 1 == d) XRS_HIP(hipMemcpyAsync(C[k], src, t.size(k) * 8, hipMemcpyDeviceToDevice, h->stream));
+    }
+    // orthogonality check of the new cores 1..d-1 (Grams into the now free Hs buffers)
+    DevIdArgs da{};
+    DevBuf dev(h, d * 8 + 64);
+    int nchk = 0;
+    for (size_t k = 1; k < d; ++k) {
+        const size_t a = t.r[k], cols = t.cols_right(k);
+        gemm(h, Hs[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
+        da.G[nchk] = Hs[k].d();
+        da.n[nchk] = int(a);
+        ++nchk;
+    }
+    da.out = dev.d();
+    hipLaunchKernelGGL(k_dev_identity_many, dim3(nchk), dim3(256), 0, h->stream, da);
+    check_launch("k_dev_identity_many");
+    double* hd = static_cast<double*>(h->host_scratch) + 64;
+    XRS_HIP(hipMemcpyAsync(hd, dev.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    bool ok = true;
+    for (int i = 0; i < nchk; ++i) ok = ok && (hd[i] <= 1e-13);
+    for (size_t k = 0; k < d; ++k) t.replace(k, C[k]);
+    if (!ok) rl_sweep(t, max_ranks, eps, cX, d - 1);
     return true;
 }
 
 void truncate_edge(TT& t, size_t k, size_t max_rank, double eps);
 void orth_right(TT& t, size_t k);
 
-bool round_fast(TT& t, const size_t* max_ranks, double eps) {
-    const size_t d = t.d;
-    if (d < 2 || exceeds_maximal_ranks(t)) return false;
-    for (size_t k = 1; k < d; ++k)
-        if (t.r[k] > max_ranks[k - 1] || t.r[k] > t.cols_right(k) || t.r[k] > 256) return false;
-    const double cX = 0.5 * std::sqrt(kLeftShift);
-    if (!(eps < 0.5 * cX * 1e-5)) return false;   // LQ certificates are ~1e-6; larger eps: reference path
-    if (!left_grams_certified(t)) return false;
-    for (size_t k = d - 1; k >= 1; --k) {
+// Sequential certified right-to-left CholeskyQR sweep from edge `from` down to 1 (the unfoldings are
+// already certified on the left with constant cX); an uncertified LQ hands over to the reference
+// algorithm at that edge.
+void rl_sweep(TT& t, const size_t* max_ranks, double eps, double cX, size_t from) {
+    for (size_t k = from; k >= 1; --k) {
         const size_t m = t.r[k], nn = t.cols_right(k), prow = t.rows_left(k - 1);
         double* Q = t.alloc(m * nn);
         double* L = t.alloc(m * m);
         const OrthResult o = orthogonalize(t.h, t.core[k], m, nn, true, Q, L);
         const double c = o.certified ? cX * o.cert_ratio : 0.0;
-        if (!(c > 16.0 * 2.220446049250313e-16 && eps < 0.5 * c)) {
-            // certificate failed at edge k: edges > k are done exactly (no cut possible there); finish
-            // with the reference algorithm: left-orthogonalise cores 0..k-1 (core k absorbs), truncate.
+        if (!(m <= nn && c > 16.0 * 2.220446049250313e-16 && eps < 0.5 * c)) {
             t.release(Q);
             t.release(L);
             for (size_t j = 0; j < k; ++j) orth_right(t, j);
             for (size_t kk = k; kk >= 1; --kk) truncate_edge(t, kk, max_ranks[kk - 1], eps);
-            return true;
+            return;
         }
         double* prv = t.alloc(prow * m);
         gemm(t.h, prv, prow, m, 1.0, t.core[k - 1], m, false, m, L, m, false);
@@ -291,12 +408,11 @@ bool round_fast(TT& t, const size_t* max_ranks, double eps) {
         t.replace(k, Q);
         t.replace(k - 1, prv);
     }
-    return true;
 }
 
 void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
-    if (round_fast(t, max_ranks, eps)) return;
+    if (round_chain(t, max_ranks, eps)) return;
     // canonicalize_right (ttNetwork.cpp:638-640, 654)
     const size_t start = canonicalized ? core_pos : 0;
     for (size_t k = start; k + 1 < d; ++k) orth_right(t, k);
