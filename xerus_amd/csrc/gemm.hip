@@ -12,6 +12,10 @@
 // (bitwise reproducible), used when the M x N tile grid alone cannot fill 256 CUs (TT shapes:
 // 256 x 256 outputs with K = n*r up to 10240).
 #include <algorithm>
+#include <type_traits>
+#include <utility>
+#include <cstdio>
+#include <cstdlib>
 
 #include "runtime.hpp"
 
@@ -19,20 +23,26 @@ namespace xrs {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int GBK = 16;
-
-template <int BM, int BN, bool TA, bool TB>
-__global__ void __launch_bounds__(256)
+template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB>
+__global__ void __launch_bounds__(WGM * WGN * WGK * 64, (WGM * WGN * WGK * 64 * 2 <= 1024) ? 2 : 1)
 k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ B, size_t ldb,
            double* __restrict__ C, int M, int N, int K, int kps, double alpha, double* __restrict__ slab,
-           int tiles_m) {
-    constexpr int SA = BM + 17;
-    constexpr int SB = BN + 17;
-    constexpr int WM = BM / 2, WN = BN / 2;
+           int tiles_m, int xcd_group) {
+    constexpr int NT = WGM * WGN * WGK * 64;   // WGK wave groups split every K-step's MFMA k-substeps
+    // LDS rows of BM / BN doubles, XOR-swizzled per k row: element (k, m) at k*SA + (m ^ swz(k)) with
+    // swz(k) = 16*(k&1) + (k>>1). Fragment reads (lanes: 16 m x rows k, k+1) hit 32 distinct bank pairs
+    // and the transposed stores (lanes: 16 consecutive k, one m) 16 distinct ones.
+    constexpr int SA = BM;
+    constexpr int SB = BN;
+    static_assert(BM % 32 == 0 && BN % 32 == 0, "swizzle needs 32-aligned tile rows");
+    constexpr int WM = BM / WGM, WN = BN / WGN;
     constexpr int TM = WM / 16, TN = WN / 16;
+    static_assert(TM >= 1 && TN >= 1, "wave tile smaller than one MFMA tile");
+    // two accumulator sets (even / odd k-substeps) when the wave tile is small: independent MFMA chains
+    constexpr int NACC = (TM * TN <= 2) ? 2 : 1;
     // per-thread staging counts (in doubles)
-    constexpr int A_PER = BM * GBK / 256;
-    constexpr int B_PER = BN * GBK / 256;
+    constexpr int A_PER = (BM * GBK + NT - 1) / NT;
+    constexpr int B_PER = (BN * GBK + NT - 1) / NT;
 
     __shared__ double As[2][GBK * SA];
     __shared__ double Bs[2][GBK * SB];
@@ -40,102 +50,187 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int wm = (wave >> 1) * WM;
-    const int wn = (wave & 1) * WN;
+    const int kg = wave / (WGM * WGN);
+    const int pos = wave % (WGM * WGN);
+    const int wm = (pos / WGN) * WM;
+    const int wn = (pos % WGN) * WN;
+    static_assert(GBK % (4 * WGK) == 0, "K-step must split evenly over the wave groups");
+    static_assert(WGK == 1 || (WGK - 1) * BM * BN <= 2 * GBK * (SA + SB), "LDS reduction buffer too small");
 
-    const int tm = blockIdx.x % tiles_m;
-    const int tn = blockIdx.x / tiles_m;
+    // XCD-aware tile order: workgroups b, b+8, b+16, ... share an XCD (round-robin dispatch), so the
+    // tiles that read the same panel of the LARGE operand are given ids congruent mod 8 and that panel
+    // is fetched into one XCD's L2 once instead of once per XCD. xcd_group: 1 = tiles sharing a B column
+    // panel (same tn) together, 2 = tiles sharing an A row panel (same tm), 0 = plain column-major order.
+    int tm, tn;
+    {
+        const int b = blockIdx.x, tiles_n = gridDim.x / tiles_m;
+        if (xcd_group == 1) {
+            const int xcd = b & 7, slot = b >> 3;
+            tn = (slot / tiles_m) * 8 + xcd;
+            tm = slot % tiles_m;
+        } else if (xcd_group == 2) {
+            const int xcd = b & 7, slot = b >> 3;
+            tm = (slot / tiles_n) * 8 + xcd;
+            tn = slot % tiles_n;
+        } else {
+            tm = b % tiles_m;
+            tn = b / tiles_m;
+        }
+    }
     const int m0 = tm * BM, n0 = tn * BN;
     const int kbeg = blockIdx.z * kps;
     const int kend = min(K, kbeg + kps);
 
-    d4 acc[TM][TN];
+    d4 acc2[NACC][TM][TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int a = 0; a < NACC; ++a)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc2[a][i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    auto swz = [](int k) { return ((k & 1) << 4) | ((k >> 1) & 15); };
 
-    double ra[A_PER], rb[B_PER];
+    // register ring: the global loads of K-step t+PD are issued while step t computes, so PD steps of
+    // MFMA work cover the global-memory latency (one step is only ~4-8 MFMAs per wave)
+    double ra[PD][A_PER], rb[PD][B_PER];
 
-    // ---- global -> registers for the K-step starting at k0
-    auto load_tile = [&](int k0) {
+    // ---- global -> registers for the K-step starting at k0. Loads are unconditional (clamped addresses)
+    // so that no branch separates them from their use and the waitcnt pass can count them; the
+    // out-of-range elements are zeroed when the slot is written to LDS.
+    auto a_coord = [&](int e, int& m, int& k) {
+        const int idx = tid + e * NT;
+        if (TA) { m = idx % BM; k = idx / BM; } else { k = idx % GBK; m = idx / GBK; }
+    };
+    auto b_coord = [&](int e, int& n, int& k) {
+        const int idx = tid + e * NT;
+        if (TB) { k = idx % GBK; n = idx / GBK; } else { n = idx % BN; k = idx / BN; }
+    };
+    auto load_tile = [&](int k0, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
 #pragma unroll
         for (int e = 0; e < A_PER; ++e) {
-            const int idx = tid + e * 256;
             int m, k;
-            if (TA) {  // A stored K x M: contiguous along m
-                m = idx % BM; k = idx / BM;
-            } else {   // A stored M x K: contiguous along k
-                k = idx % GBK; m = idx / GBK;
-            }
-            const int gm = m0 + m, gk = k0 + k;
-            double v = 0.0;
-            if (gm < M && gk < kend) v = TA ? A[size_t(gk) * lda + gm] : A[size_t(gm) * lda + gk];
-            ra[e] = v;
+            a_coord(e, m, k);
+            const int gm = min(m0 + m, M - 1), gk = min(k0 + k, kend - 1);
+            ra[slot][e] = TA ? A[size_t(gk) * lda + gm] : A[size_t(gm) * lda + gk];
         }
 #pragma unroll
         for (int e = 0; e < B_PER; ++e) {
-            const int idx = tid + e * 256;
             int n, k;
-            if (TB) {  // B stored N x K: contiguous along k
-                k = idx % GBK; n = idx / GBK;
-            } else {   // B stored K x N: contiguous along n
-                n = idx % BN; k = idx / BN;
-            }
-            const int gn = n0 + n, gk = k0 + k;
-            double v = 0.0;
-            if (gn < N && gk < kend) v = TB ? B[size_t(gn) * ldb + gk] : B[size_t(gk) * ldb + gn];
-            rb[e] = v;
+            b_coord(e, n, k);
+            const int gn = min(n0 + n, N - 1), gk = min(k0 + k, kend - 1);
+            rb[slot][e] = TB ? B[size_t(gn) * ldb + gk] : B[size_t(gk) * ldb + gn];
         }
     };
-    auto store_tile = [&](int buf) {
+    auto store_tile = [&](int buf, int k0, auto slot_c) {
+        constexpr int slot = decltype(slot_c)::value;
 #pragma unroll
         for (int e = 0; e < A_PER; ++e) {
-            const int idx = tid + e * 256;
             int m, k;
-            if (TA) { m = idx % BM; k = idx / BM; } else { k = idx % GBK; m = idx / GBK; }
-            As[buf][k * SA + m] = ra[e];
+            a_coord(e, m, k);
+            const bool ok = (m0 + m < M) && (k0 + k < kend);
+            if (tid + e * NT < BM * GBK) As[buf][k * SA + (m ^ swz(k))] = ok ? ra[slot][e] : 0.0;
         }
 #pragma unroll
         for (int e = 0; e < B_PER; ++e) {
-            const int idx = tid + e * 256;
             int n, k;
-            if (TB) { k = idx % GBK; n = idx / GBK; } else { n = idx % BN; k = idx / BN; }
-            Bs[buf][k * SB + n] = rb[e];
+            b_coord(e, n, k);
+            const bool ok = (n0 + n < N) && (k0 + k < kend);
+            if (tid + e * NT < BN * GBK) Bs[buf][k * SB + (n ^ swz(k))] = ok ? rb[slot][e] : 0.0;
+        }
+    };
+    const int lr = lane & 15, lk = lane >> 4;
+    auto compute = [&](int buf) {
+        const double* as = As[buf];
+        const double* bs = Bs[buf];
+#pragma unroll
+        for (int q = 0; q < GBK / (4 * WGK); ++q) {
+            const int kk = (q * WGK + kg) * 4;
+            double af[TM], bf[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = as[(kk + lk) * SA + ((wm + i * 16 + lr) ^ swz(kk + lk))];
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bf[j] = bs[(kk + lk) * SB + ((wn + j * 16 + lr) ^ swz(kk + lk))];
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc2[q % NACC][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc2[q % NACC][i][j], 0, 0, 0);
         }
     };
 
     const int nsteps = (kend > kbeg) ? (kend - kbeg + GBK - 1) / GBK : 0;
     if (nsteps > 0) {
-        load_tile(kbeg);
-        store_tile(0);
+        static_assert(PD % 2 == 0, "ring depth must be even (LDS double buffer parity)");
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            ((U < nsteps ? load_tile(kbeg + U * GBK, std::integral_constant<int, U>{}) : void()), ...);
+        }(std::make_integer_sequence<int, PD>{});
+        store_tile(0, kbeg, std::integral_constant<int, 0>{});
         __syncthreads();
-        const int lr = lane & 15, lk = lane >> 4;
-        for (int s = 0; s < nsteps; ++s) {
-            const int cur = s & 1;
-            if (s + 1 < nsteps) load_tile(kbeg + (s + 1) * GBK);
-            const double* as = As[cur];
-            const double* bs = Bs[cur];
-#pragma unroll
-            for (int kk = 0; kk < GBK; kk += 4) {
-                double af[TM], bf[TN];
-#pragma unroll
-                for (int i = 0; i < TM; ++i) af[i] = as[(kk + lk) * SA + wm + i * 16 + lr];
-#pragma unroll
-                for (int j = 0; j < TN; ++j) bf[j] = bs[(kk + lk) * SB + wn + j * 16 + lr];
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[i], bf[j], acc[i][j], 0, 0, 0);
-            }
-            if (s + 1 < nsteps) {
-                store_tile(cur ^ 1);
-            }
-            __syncthreads();
+        int t0 = 0;
+        // steady state: no guards, every iteration issues the loads of step t + PD
+        for (; t0 + 2 * PD <= nsteps; t0 += PD) {
+            [&]<int... U>(std::integer_sequence<int, U...>) {
+                (([&] {
+                     const int t = t0 + U;
+                     compute(U & 1);
+                     store_tile((U + 1) & 1, kbeg + (t + 1) * GBK, std::integral_constant<int, (U + 1) % PD>{});
+                     load_tile(kbeg + (t + PD) * GBK, std::integral_constant<int, U>{});
+                     __syncthreads();
+                 }()),
+                 ...);
+            }(std::make_integer_sequence<int, PD>{});
+        }
+        // tail
+        for (; t0 < nsteps; t0 += PD) {
+            [&]<int... U>(std::integer_sequence<int, U...>) {
+                (([&] {
+                     const int t = t0 + U;
+                     if (t < nsteps) {
+                         compute(U & 1);
+                         if (t + 1 < nsteps)
+                             store_tile((U + 1) & 1, kbeg + (t + 1) * GBK, std::integral_constant<int, (U + 1) % PD>{});
+                         if (t + PD < nsteps) load_tile(kbeg + (t + PD) * GBK, std::integral_constant<int, U>{});
+                     }
+                     __syncthreads();
+                 }()),
+                 ...);
+            }(std::make_integer_sequence<int, PD>{});
         }
     }
 
+    d4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            acc[i][j] = acc2[0][i][j];
+            if constexpr (NACC > 1) acc[i][j] += acc2[1][i][j];
+        }
+    // ---- intra-workgroup K reduction (wave groups 1.. -> LDS -> group 0)
+    if constexpr (WGK > 1) {
+        double* red = &As[0][0];
+        if (kg > 0) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        red[((((kg - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+        }
+        __syncthreads();
+        if (kg > 0) return;
+#pragma unroll
+        for (int g = 1; g < WGK; ++g)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i][j][r] += red[((((g - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane];
+    }
     // ---- epilogue
     const bool to_slab = slab != nullptr;
     double* out = to_slab ? slab + size_t(blockIdx.z) * size_t(M) * size_t(N) : C;
@@ -164,16 +259,21 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(double* __restrict__ C, c
     }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD>
 static void launch_tiles(xrs_handle_t h, const double* A, size_t lda, bool ta, const double* B, size_t ldb, bool tb,
                          double* C, int M, int N, int K, int splits, int kps, double alpha, double* slab) {
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     dim3 grid(unsigned(tiles_m * tiles_n), 1, unsigned(splits));
+    // group by the larger operand's panels (B: K x N, A: M x K) when the tile grid allows a bijection
+    int xg = 0;
+    if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
+    else xg = (tiles_m % 8 == 0) ? 2 : 0;
+    if (std::getenv("XRS_GEMM_NOXCD")) xg = 0;
     KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(M) * double(N) * double(K),
                       8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GEMM_LAUNCH(TA_, TB_)                                                                             \
-    hipLaunchKernelGGL((k_gemm_f64<BM, BN, TA_, TB_>), grid, dim3(256), 0, h->stream, A, lda, B, ldb, C, M, N, K, \
-                       kps, alpha, slab, tiles_m)
+    hipLaunchKernelGGL((k_gemm_f64<BM, BN, GBK, WGM, WGN, WGK, PD, TA_, TB_>), grid, dim3(WGM * WGN * WGK * 64), 0, h->stream, A, lda, B, ldb, C, M, N, K, \
+                       kps, alpha, slab, tiles_m, xg)
     if (!ta && !tb) XRS_GEMM_LAUNCH(false, false);
     else if (!ta && tb) XRS_GEMM_LAUNCH(false, true);
     else if (ta && !tb) XRS_GEMM_LAUNCH(true, false);
@@ -191,27 +291,49 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
         XRS_HIP(hipMemsetAsync(C, 0, size_t(M) * N * 8, h->stream));
         return;
     }
-    // tile choice: 128x128 when that alone yields >= 256 tiles, else 64x64 (+ split-K)
-    const long t128 = long((M + 127) / 128) * ((N + 127) / 128);
-    const long t64 = long((M + 63) / 64) * ((N + 63) / 64);
-    const bool big = t128 >= 240;
-    const long tiles = big ? t128 : t64;
+    // Tile choice (XRS_GEMM_CFG="variant,kmin,target" overrides for tuning experiments):
+    //   v1 128x128 (8 waves 2x4)              large problems (>= 240 tiles)
+    //   v2  64x64  (8 waves 2x4)              mid-size
+    //   v3  64x32  (8 waves 2x2, K split 2)   TT "wide" shapes (M or N = r, other = n r): 2.5 tiles per CU
+    //   v4  32x32  (8 waves 2x2, K split 2)   + split-K for the r x r Gram shapes with K = n r
+    // split-K brings the grid to ~target workgroups while every split keeps >= kmin of K.
+    static int cfg_var = 0, cfg_kmin = 256, cfg_target = 512;
+    static bool cfg_read = false;
+    if (!cfg_read) {
+        cfg_read = true;
+        if (const char* e = std::getenv("XRS_GEMM_CFG")) std::sscanf(e, "%d,%d,%d", &cfg_var, &cfg_kmin, &cfg_target);
+    }
+    auto ntiles = [&](int bm, int bn) { return long((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+    int var = cfg_var;
+    if (var == 0) {
+        if (ntiles(128, 128) >= 240) var = 1;
+        else if (ntiles(64, 64) >= 512) var = 2;
+        else if (ntiles(64, 32) >= 256) var = 3;
+        else var = 4;
+    }
+    const int bms[8] = {0, 128, 64, 64, 32, 64, 64, 64}, bns[8] = {0, 128, 64, 32, 32, 32, 64, 64};
+    const long tiles = ntiles(bms[var], bns[var]);
     int splits = 1;
-    if (tiles < 256) {
-        // split K so that tiles*splits ~ 256-512 blocks while each split keeps >= 128 of K
-        const long want = (512 + tiles - 1) / tiles;
-        const long maxs = std::max<long>(1, K / 128);
+    if (tiles < cfg_target) {
+        const long want = (cfg_target + tiles - 1) / tiles;
+        const long maxs = std::max<long>(1, K / cfg_kmin);
         splits = int(std::max<long>(1, std::min(want, maxs)));
     }
+    const int bk = (var >= 5) ? 32 : 16;
     int kps = (K + splits - 1) / splits;
-    kps = (kps + GBK - 1) / GBK * GBK;
+    kps = (kps + bk - 1) / bk * bk;
     splits = (K + kps - 1) / kps;
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(splits) * M * N * sizeof(double));
-    if (big)
-        launch_tiles<128, 128>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d());
-    else
-        launch_tiles<64, 64>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d());
+    switch (var) {
+        case 1: launch_tiles<128, 128, 16, 2, 4, 1, 2>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        case 2: launch_tiles<64, 64, 16, 2, 4, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        case 3: launch_tiles<64, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        case 5: launch_tiles<64, 32, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        case 6: launch_tiles<64, 64, 32, 2, 2, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        case 7: launch_tiles<64, 64, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        default: launch_tiles<32, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+    }
     if (splits > 1) {
         const size_t MN = size_t(M) * N;
         const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));

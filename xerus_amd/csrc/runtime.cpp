@@ -121,6 +121,36 @@ extern "C" {
 const char* xrs_last_error(void) { return g_last_error.c_str(); }
 const char* xrs_version(void) { return "xerus_amd 0.1 (gfx950)"; }
 
+StreamFork::StreamFork(xrs_handle_t h) : h_(h), main_stream_(h->stream), main_pool_(h->pool) {
+    XRS_HIP(hipEventRecord(h_->ev_fork, main_stream_));
+    XRS_HIP(hipStreamWaitEvent(h_->side_stream, h_->ev_fork, 0));
+}
+
+void StreamFork::side() {
+    h_->stream = h_->side_stream;
+    h_->pool = h_->side_pool;
+}
+
+void StreamFork::main() {
+    h_->stream = main_stream_;
+    h_->pool = main_pool_;
+}
+
+void StreamFork::join() {
+    if (joined_) return;
+    joined_ = true;
+    main();
+    XRS_HIP(hipEventRecord(h_->ev_join, h_->side_stream));
+    XRS_HIP(hipStreamWaitEvent(main_stream_, h_->ev_join, 0));
+}
+
+StreamFork::~StreamFork() {
+    try {
+        join();
+    } catch (...) {
+    }
+}
+
 int xrs_create(xrs_handle_t* handle, int device) {
     return guarded([&] {
         XRS_REQUIRE(handle != nullptr, "null handle pointer");
@@ -133,6 +163,10 @@ int xrs_create(xrs_handle_t* handle, int device) {
         XRS_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
         h->stream = h->own_stream;
         h->pool = new Pool(device);
+        XRS_HIP(hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
+        h->side_pool = new Pool(device);
+        XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+        XRS_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
         *handle = h;
@@ -149,7 +183,12 @@ int xrs_destroy(xrs_handle_t h) {
             (void)hipEventDestroy(r.stop);
         }
         for (auto e : h->event_cache) (void)hipEventDestroy(e);
+        if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
         delete h->pool;
+        delete h->side_pool;
+        if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
+        if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+        if (h->ev_join) (void)hipEventDestroy(h->ev_join);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);

@@ -88,6 +88,10 @@ struct xrs_handle_s {
     void* host_scratch = nullptr;
     // device scratch for reductions / statuses (64 KiB)
     void* dev_scratch = nullptr;
+    // side stream (+ its own stream-ordered pool) for independent work forked from `stream`
+    hipStream_t side_stream = nullptr;
+    xrs::Pool* side_pool = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // profiler
     uint32_t prof_mask = 0;
     std::vector<xrs::ProfRecord> prof;
@@ -133,5 +137,22 @@ class KernelTimer {
 };
 
 void check_launch(const char* what);
+
+// Fork/join of independent work onto the handle's side stream. While `side()` is active every launch
+// and DevBuf of the handle goes to the side stream / side pool (stream-ordered reuse stays valid);
+// buffers shared across the fork must be allocated before it and released after join().
+class StreamFork {
+   public:
+    explicit StreamFork(xrs_handle_t h);
+    ~StreamFork();
+    void side();   // switch to the side stream (after the fork point)
+    void main();   // switch back
+    void join();   // main stream waits for the side stream's work
+   private:
+    xrs_handle_t h_;
+    hipStream_t main_stream_;
+    Pool* main_pool_;
+    bool joined_ = false;
+};
 
 }  // namespace xrs

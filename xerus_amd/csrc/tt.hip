@@ -223,41 +223,51 @@ constexpr double kGramShift = 1e-9;
 // Gram chains from the current cores (k = 1..d-1, index k):
 //   left  G_k = X_{<k}^T X_{<k}:  G_1 = M_0^T M_0, G_{k+1} = M_k^T (G_k M_k)   (M_k: r_k x n_k r_{k+1})
 //   right H_k = X_{>=k} X_{>=k}^T: H_{d-1} = M M^T, H_k = M_k (I (x) H_{k+1}) M_k^T
-void left_grams(TT& t, std::vector<DevBuf>& G) {
+void left_grams(TT& t, std::vector<DevBuf>& G, double* T) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
-    G.clear();
-    G.resize(d);
-    size_t tmax = 1;
-    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
-    DevBuf T(h, tmax * 8);
-    G[1] = DevBuf(h, t.r[1] * t.r[1] * 8);
     gemm(h, G[1].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
     for (size_t k = 1; k + 1 < d; ++k) {
         const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-        gemm(h, T.d(), a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
-        G[k + 1] = DevBuf(h, b * b * 8);
-        gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T.d(), b, false);
+        gemm(h, T, a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
+        gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);
     }
 }
 
-void right_grams(TT& t, std::vector<DevBuf>& H) {
+void right_grams(TT& t, std::vector<DevBuf>& H, double* T) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
+    const size_t last = d - 1, cl = t.cols_right(last);
+    gemm(h, H[last].d(), t.r[last], t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
+    for (size_t k = last - 1; k >= 1; --k) {
+        const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
+        gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
+        gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T, cols, true);         // M_k T^T
+    }
+}
+
+// Both chains, concurrently: left on the side stream, right on the main stream (independent inputs;
+// every buffer they touch is allocated before the fork and outlives the join).
+void gram_chains(TT& t, std::vector<DevBuf>& G, std::vector<DevBuf>& H) {
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    G.clear();
     H.clear();
+    G.resize(d);
     H.resize(d);
     size_t tmax = 1;
     for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
-    DevBuf T(h, tmax * 8);
-    const size_t last = d - 1, rl = t.r[last], cl = t.cols_right(last);
-    H[last] = DevBuf(h, rl * rl * 8);
-    gemm(h, H[last].d(), rl, rl, 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
-    for (size_t k = last - 1; k >= 1; --k) {
-        const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-        gemm(h, T.d(), a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
-        H[k] = DevBuf(h, a * a * 8);
-        gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T.d(), cols, true);         // M_k T^T
+    for (size_t k = 1; k < d; ++k) {
+        G[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
+        H[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
     }
+    DevBuf TL(h, tmax * 8), TR(h, tmax * 8);
+    StreamFork fork(h);
+    fork.side();
+    left_grams(t, G, TL.d());
+    fork.main();
+    right_grams(t, H, TR.d());
+    fork.join();
 }
 
 struct DevIdArgs {
@@ -272,7 +282,7 @@ __global__ void __launch_bounds__(256) k_dev_identity_many(const DevIdArgs args)
     const int n = args.n[blockIdx.x];
     __shared__ double red[4];
     double mx = 0.0;
-    for (int e = threadIdx.x; e < n * n; e += 256) {
+    for (int e = threadIdx.x + 256 * blockIdx.y; e < n * n; e += 256 * gridDim.y) {
         const double v = fabs(G[e] - ((e / n) == (e % n) ? 1.0 : 0.0));
         mx = (v > mx || v != v) ? v : mx;
     }
@@ -286,7 +296,7 @@ __global__ void __launch_bounds__(256) k_dev_identity_many(const DevIdArgs args)
     if (threadIdx.x == 0) {
         double m = red[0];
         for (int i = 1; i < 4; ++i) m = (red[i] > m || red[i] != red[i]) ? red[i] : m;
-        args.out[blockIdx.x] = m;
+        args.out[blockIdx.x * gridDim.y + blockIdx.y] = m;
     }
 }
 
@@ -308,8 +318,7 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     const double cX = 0.5 * std::sqrt(kGramShift);
     if (!(eps < 0.25 * cX * cX)) return false;
     std::vector<DevBuf> G, H, Hs;
-    left_grams(t, G);
-    right_grams(t, H);
+    gram_chains(t, G, H);
     Hs.resize(d);
     const int cnt = int(3 * (d - 1));
     DevBuf Dv(h, (d - 1) * 256 * 16 * 8 + 8), Dscr(h, 2 * (d - 1) * 256 * 16 * 8 + 8), st(h, size_t(cnt) * 4 + 64);
@@ -360,7 +369,7 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     }
     // orthogonality check of the new cores 1..d-1 (Grams into the now free Hs buffers)
     DevIdArgs da{};
-    DevBuf dev(h, d * 8 + 64);
+    DevBuf dev(h, d * 16 * 8 + 64);
     int nchk = 0;
     for (size_t k = 1; k < d; ++k) {
         const size_t a = t.r[k], cols = t.cols_right(k);
@@ -370,13 +379,14 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
         ++nchk;
     }
     da.out = dev.d();
-    hipLaunchKernelGGL(k_dev_identity_many, dim3(nchk), dim3(256), 0, h->stream, da);
+    constexpr int kSlices = 16;
+    hipLaunchKernelGGL(k_dev_identity_many, dim3(nchk, kSlices), dim3(256), 0, h->stream, da);
     check_launch("k_dev_identity_many");
     double* hd = static_cast<double*>(h->host_scratch) + 64;
-    XRS_HIP(hipMemcpyAsync(hd, dev.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipMemcpyAsync(hd, dev.d(), size_t(nchk) * kSlices * 8, hipMemcpyDeviceToHost, h->stream));
     XRS_HIP(hipStreamSynchronize(h->stream));
     bool ok = true;
-    for (int i = 0; i < nchk; ++i) ok = ok && (hd[i] <= 1e-13);
+    for (int i = 0; i < nchk * kSlices; ++i) ok = ok && (hd[i] <= 1e-13);   // NaN fails too
     for (size_t k = 0; k < d; ++k) t.replace(k, C[k]);
     if (!ok) rl_sweep(t, max_ranks, eps, cX, d - 1);
     return true;
