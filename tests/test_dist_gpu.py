@@ -1,0 +1,94 @@
+"""Mode-sharded TT round / <x,y> through the C-ABI (xrs_tt_round_sharded, xrs_tt_dot_sharded).
+
+Two ranks share the box's single GPU (gloo all-reduce with host staging); one rank with the nccl
+(= RCCL) backend exercises the device-native all-reduce path. Parity: same ranks as the oracle's round,
+same represented tensor, <x,y> within 1e-12 ||x|| ||y||.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rel_diff(ref, a_cores, b_cores):
+    A = ref.TT([c.copy() for c in a_cores])
+    nb = [c.copy() for c in b_cores]
+    nb[0] = -nb[0]
+    D = ref.tt_add(A, ref.TT(nb))
+    D.move_core(0)
+    B = ref.TT([c.copy() for c in b_cores])
+    B.move_core(0)
+    return D.frob_norm() / B.frob_norm()
+
+
+def _worker(rank, world, port, backend, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    try:
+        from oracle import xerus_ref as ref
+        from xerus_amd import capi
+        from xerus_amd import dist as xd
+
+        torch.cuda.set_device(0)
+        h = capi.Handle(0)
+        comm = xd.TorchAllReduce()
+        dims, ranks = [8, 6, 7, 5, 8, 6], [6, 12, 12, 10, 6]
+        x = ref.TT.random_raw(dims, ranks, ref.Rng(31))
+        y = ref.TT.random_raw(dims, ranks, ref.Rng(37))
+        sx = xd.ShardedTT.from_full_cores(h, x.cores, world, rank)
+        sy = xd.ShardedTT.from_full_cores(h, y.cores, world, rank)
+        d_sh = sx.dot(sy, comm)
+        d_ref = ref.dot(x, y)
+        nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
+        cert = sx.round(12, comm)
+        full = sx.gather(dist.all_gather_object)
+        res = {"dot_err": abs(d_sh - d_ref) / (nx * ny), "cert": cert, "ranks": sx.ranks}
+        if rank == 0:
+            xr = x.copy()
+            xr.round(12)
+            res["ref_ranks"] = xr.ranks
+            res["diff"] = _rel_diff(ref, full, x.cores)
+            # right-canonical: cores 1.. have orthonormal rows
+            res["orth"] = max(np.abs(c.reshape(c.shape[0], -1) @ c.reshape(c.shape[0], -1).T - np.eye(c.shape[0])).max()
+                              for c in full[1:])
+        # doubled ranks (x + x): certificate must fail, cores untouched
+        s2 = ref.tt_add(x, x)
+        ss = xd.ShardedTT.from_full_cores(h, s2.cores, world, rank)
+        before = ss.local.cores()
+        res["cert_sum"] = ss.round(100, comm)
+        after = ss.local.cores()
+        res["untouched"] = all(np.array_equal(a, b) for a, b in zip(before, after))
+        out[rank] = res
+        h.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (1, "nccl")])
+def test_sharded_round_and_dot(world, backend):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), backend, out), nprocs=world, join=True)
+    r0 = out[0]
+    for rank in range(world):
+        r = out[rank]
+        assert r["dot_err"] <= 1e-12
+        assert r["cert"] is True
+        assert r["ranks"] == r0["ref_ranks"]
+        assert r["cert_sum"] is False and r["untouched"]
+    assert r0["diff"] <= 1e-12
+    assert r0["orth"] <= 1e-13

@@ -52,6 +52,10 @@ SIGNATURES = {
                                C.POINTER(_SZ), C.c_double]),
     "xrs_tt_dot": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                              C.POINTER(_SZ), C.POINTER(_DP)]),
+    "xrs_tt_round_sharded": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
+                                       C.c_double, _DP, _DP, C.POINTER(C.c_int)]),
+    "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
+                                     C.POINTER(_SZ), C.POINTER(_DP), _DP, _DP]),
     "xrs_prof_begin": (C.c_int, [_DP, C.c_uint32]),
     "xrs_prof_end": (C.c_int, [_DP, C.POINTER(_SZ), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                C.POINTER(C.c_double)]),

@@ -37,8 +37,8 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 //   (2) wave 1 inverts it (D^{-1}, for the TRSM kernel) while the other waves solve the panel rows
 //       x D^T = g by substitution against D in LDS (one row per thread, 32 registers);
 //   (3) all waves apply the rank-32 trailing update from the LDS panel with 4x4 register tiles.
-__global__ void __launch_bounds__(POT_THREADS) k_potrf(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
-                                                 int* __restrict__ status, double* __restrict__ info) {
+__device__ __forceinline__ void potrf32_body(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
+                                             int* __restrict__ status, double* __restrict__ info) {
     __shared__ double P[PMAX * (NB + 1)];
     __shared__ double Ds[NB][NB + 1];
     __shared__ double red[16];
@@ -208,6 +208,11 @@ __global__ void __launch_bounds__(POT_THREADS) k_potrf(double* __restrict__ G, i
         if (c > r) G[size_t(r) * n + c] = 0.0;
     }
     if (tid == 0) status[0] = fail;
+}
+
+__global__ void __launch_bounds__(POT_THREADS) k_potrf(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
+                                                 int* __restrict__ status, double* __restrict__ info) {
+    potrf32_body(G, n, shift_rel, Dinv, status, info);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -517,7 +522,12 @@ __global__ void __launch_bounds__(PR_THREADS) k_potrf_rr(double* __restrict__ G,
     potrf_rr_body(G, n, shift_rel, Dinv, status, info);
 }
 
-// Independent factorisations, one workgroup each (e.g. the left Gram matrices of every TT edge).
+// Independent factorisations, one workgroup each (e.g. the Gram matrices of every TT edge).
+__global__ void __launch_bounds__(POT_THREADS) k_potrf32_batched(PotrfBatch b) {
+    const int i = blockIdx.x;
+    potrf32_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr);
+}
+
 __global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
     const int i = blockIdx.x;
     potrf_rr_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr);
@@ -583,13 +593,18 @@ __global__ void __launch_bounds__(256) k_trsm16(const double* __restrict__ L, co
         d4 y;
 #pragma unroll
         for (int q = 0; q < 4; ++q) y[q] = Xs[(16 * I + lg + 4 * q) * PT + lr];
-        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        // one accumulator per J tile: independent MFMA chains (a single chain is latency-bound)
+        d4 accj[JS];
 #pragma unroll
         for (int js = 0; js < JS; ++js) {
+            accj[js] = d4{0.0, 0.0, 0.0, 0.0};
             if (wave + 4 * js >= I) continue;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(la[js][c], xr[js][c], acc, 0, 0, 0);
+            for (int c = 0; c < 4; ++c) accj[js] = __builtin_amdgcn_mfma_f64_16x16x4f64(la[js][c], xr[js][c], accj[js], 0, 0, 0);
         }
+        d4 acc = accj[0];
+#pragma unroll
+        for (int js = 1; js < JS; ++js) acc += accj[js];
         double* rb = red[I & 1][0];
 #pragma unroll
         for (int q = 0; q < 4; ++q) rb[wave * 256 + q * 64 + lane] = acc[q];
@@ -598,9 +613,12 @@ __global__ void __launch_bounds__(256) k_trsm16(const double* __restrict__ L, co
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             t[q] = y[q] - ((rb[q * 64 + lane] + rb[256 + q * 64 + lane]) + (rb[512 + q * 64 + lane] + rb[768 + q * 64 + lane]));
-        d4 x = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) x = __builtin_amdgcn_mfma_f64_16x16x4f64(da[c], t[c], x, 0, 0, 0);
+        d4 x0 = {0.0, 0.0, 0.0, 0.0}, x1 = {0.0, 0.0, 0.0, 0.0};
+        x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(da[0], t[0], x0, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(da[1], t[1], x1, 0, 0, 0);
+        x0 = __builtin_amdgcn_mfma_f64_16x16x4f64(da[2], t[2], x0, 0, 0, 0);
+        x1 = __builtin_amdgcn_mfma_f64_16x16x4f64(da[3], t[3], x1, 0, 0, 0);
+        const d4 x = x0 + x1;
         if ((I & 3) == wave) {
 #pragma unroll
             for (int js = 0; js < JS; ++js)
@@ -928,6 +946,7 @@ __global__ void __launch_bounds__(1024) k_svd_finish(const double* __restrict__ 
 // ------------------------------------------------------------------------------------------------ launchers
 // Dinv row stride: k_potrf_rr (n <= 256) writes 16x16 blocks, k_potrf 32x32 blocks.
 static int dinv_ld(int n) { return n <= PR_TMAX * 16 ? 16 : 32; }
+size_t dinv_elems(int n) { return dinv_ld(n) == 16 ? size_t((n + 15) / 16) * 256 : size_t(n + 32) * 32; }
 
 void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int* status_dev, double* info_dev) {
     XRS_REQUIRE(n >= 1 && n <= PMAX, "potrf: n out of range for the single-workgroup kernel");
@@ -944,12 +963,48 @@ void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int
 void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count) {
     XRS_REQUIRE(count >= 0 && count <= kPotrfBatchMax, "potrf_batched: batch too large");
     if (count == 0) return;
-    for (int i = 0; i < count; ++i) XRS_REQUIRE(b.n[i] >= 1 && b.n[i] <= PR_TMAX * 16, "potrf_batched: n out of range");
-    double fl = 0.0;
-    for (int i = 0; i < count; ++i) fl += double(b.n[i]) * b.n[i] * b.n[i] / 3.0;
-    KernelTimer timer(h, XRS_KFAM_QR, fl, 0.0);
-    hipLaunchKernelGGL(k_potrf_rr_batched, dim3(count), dim3(PR_THREADS), 0, h->stream, b);
-    check_launch("k_potrf_rr_batched");
+    // n <= 256: register-resident kernel (16-block Dinv); larger (<= 512): 32-block kernel. One launch
+    // per kind, each entry's Dinv layout matching dinv_ld(n) (what trsm() expects).
+    PotrfBatch small{}, large{};
+    int ns = 0, nl = 0;
+    double fl_s = 0.0, fl_l = 0.0;
+    for (int i = 0; i < count; ++i) {
+        XRS_REQUIRE(b.n[i] >= 1 && b.n[i] <= PMAX, "potrf_batched: n out of range");
+        const bool rr = dinv_ld(b.n[i]) == 16;
+        PotrfBatch& d = rr ? small : large;
+        int& c = rr ? ns : nl;
+        d.G[c] = b.G[i];
+        d.Dinv[c] = b.Dinv[i];
+        d.shift[c] = b.shift[i];
+        d.n[c] = b.n[i];
+        (rr ? fl_s : fl_l) += double(b.n[i]) * b.n[i] * b.n[i] / 3.0;
+        ++c;
+    }
+    // statuses: written back in the caller's order through a small device copy
+    DevBuf st(h, size_t(count) * 4 + 64);
+    small.status = st.as<int>();
+    large.status = st.as<int>() + ns;
+    if (ns) {
+        KernelTimer timer(h, XRS_KFAM_QR, fl_s, 0.0);
+        hipLaunchKernelGGL(k_potrf_rr_batched, dim3(ns), dim3(PR_THREADS), 0, h->stream, small);
+        check_launch("k_potrf_rr_batched");
+    }
+    if (nl) {
+        KernelTimer timer(h, XRS_KFAM_QR, fl_l, 0.0);
+        hipLaunchKernelGGL(k_potrf32_batched, dim3(nl), dim3(POT_THREADS), 0, h->stream, large);
+        check_launch("k_potrf32_batched");
+    }
+    if (nl == 0) {
+        XRS_HIP(hipMemcpyAsync(b.status, st.d(), size_t(count) * 4, hipMemcpyDeviceToDevice, h->stream));
+    } else {
+        // restore the caller's order (small entries first in st)
+        int is = 0, il = 0;
+        for (int i = 0; i < count; ++i) {
+            const bool rr = dinv_ld(b.n[i]) == 16;
+            const int src = rr ? is++ : ns + il++;
+            XRS_HIP(hipMemcpyAsync(b.status + i, st.as<int>() + src, 4, hipMemcpyDeviceToDevice, h->stream));
+        }
+    }
 }
 
 void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n, const double* Y, size_t ldy, double* X,

@@ -21,6 +21,8 @@ struct PotrfBatch {
     int* status;
 };
 void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count);
+// doubles needed for the Dinv output of potrf / potrf_batched for an n x n matrix
+size_t dinv_elems(int n);
 // X = L^{-1} Y. cols=false: the RHS vectors are the nvec rows of Y (ld ldy); cols=true: the nvec columns.
 void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n, const double* Y, size_t ldy, double* X,
           size_t ldx, int nvec);

@@ -40,6 +40,18 @@ struct TT {
     double* alloc(size_t elems) { return static_cast<double*>(h->pool->alloc(std::max<size_t>(elems, 1) * 8)); }
     void release(double* p) { if (p) h->pool->release(p); }
     void replace(size_t k, double* p) { release(core[k]); core[k] = p; }
+
+    // Mode-sharded TT (xrs_tt_*_sharded): n[] are this rank's slice counts and every sum over the
+    // mode index is completed by an all-reduce across ranks; null for a whole TT on one device.
+    xrs_allreduce_fn ar = nullptr;
+    void* ar_ctx = nullptr;
+    bool sharded() const { return ar != nullptr; }
+    void reduce(double* buf, size_t count) const {
+        if (!ar) return;
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        const int rc = ar(ar_ctx, buf, count);
+        XRS_REQUIRE(rc == 0, "all-reduce callback failed");
+    }
 };
 
 // reduce_to_maximal_ranks (ttNetwork.cpp:370-402)
@@ -227,10 +239,12 @@ void left_grams(TT& t, std::vector<DevBuf>& G, double* T) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
     gemm(h, G[1].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
+    t.reduce(G[1].d(), t.r[1] * t.r[1]);
     for (size_t k = 1; k + 1 < d; ++k) {
         const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
         gemm(h, T, a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
         gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);
+        t.reduce(G[k + 1].d(), b * b);
     }
 }
 
@@ -239,10 +253,12 @@ void right_grams(TT& t, std::vector<DevBuf>& H, double* T) {
     xrs_handle_t h = t.h;
     const size_t last = d - 1, cl = t.cols_right(last);
     gemm(h, H[last].d(), t.r[last], t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
+    t.reduce(H[last].d(), t.r[last] * t.r[last]);
     for (size_t k = last - 1; k >= 1; --k) {
         const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
         gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
         gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T, cols, true);         // M_k T^T
+        t.reduce(H[k].d(), a * a);
     }
 }
 
@@ -262,6 +278,11 @@ void gram_chains(TT& t, std::vector<DevBuf>& G, std::vector<DevBuf>& H) {
         H[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
     }
     DevBuf TL(h, tmax * 8), TR(h, tmax * 8);
+    if (t.sharded()) {   // the all-reduce hook synchronises: keep the chains on one stream
+        left_grams(t, G, TL.d());
+        right_grams(t, H, TR.d());
+        return;
+    }
     StreamFork fork(h);
     fork.side();
     left_grams(t, G, TL.d());
@@ -312,27 +333,31 @@ void rl_sweep(TT& t, const size_t* max_ranks, double eps, double cX, size_t from
 bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
-    if (d < 2 || d > 65 || exceeds_maximal_ranks(t)) return false;
+    if (d < 2 || d > 65 || (!t.sharded() && exceeds_maximal_ranks(t))) return false;
     for (size_t k = 1; k < d; ++k)
-        if (t.r[k] > max_ranks[k - 1] || t.r[k] > 256) return false;
+        if (t.r[k] > max_ranks[k - 1] || t.r[k] > size_t(kSmallMax)) return false;
     const double cX = 0.5 * std::sqrt(kGramShift);
     if (!(eps < 0.25 * cX * cX)) return false;
     std::vector<DevBuf> G, H, Hs;
     gram_chains(t, G, H);
     Hs.resize(d);
     const int cnt = int(3 * (d - 1));
-    DevBuf Dv(h, (d - 1) * 256 * 16 * 8 + 8), Dscr(h, 2 * (d - 1) * 256 * 16 * 8 + 8), st(h, size_t(cnt) * 4 + 64);
+    size_t dsz = 0;
+    for (size_t k = 1; k < d; ++k) dsz += dinv_elems(int(t.r[k]));
+    DevBuf Dv(h, dsz * 8 + 8), Dscr(h, 2 * dsz * 8 + 8), st(h, size_t(cnt) * 4 + 64);
     std::vector<double*> dinv(d, nullptr);
     struct Job { double* G; double* Dinv; double shift; int n; };
     std::vector<Job> jobs;
+    size_t off = 0;
     for (size_t k = 1; k < d; ++k) {
-        const size_t a = t.r[k];
+        const size_t a = t.r[k], de = dinv_elems(int(a));
         Hs[k] = DevBuf(h, a * a * 8);
         XRS_HIP(hipMemcpyAsync(Hs[k].d(), H[k].d(), a * a * 8, hipMemcpyDeviceToDevice, h->stream));
-        dinv[k] = Dv.d() + (k - 1) * 256 * 16;
+        dinv[k] = Dv.d() + off;
         jobs.push_back({H[k].d(), dinv[k], 0.0, int(a)});
-        jobs.push_back({G[k].d(), Dscr.d() + (2 * (k - 1)) * 256 * 16, -kGramShift, int(a)});
-        jobs.push_back({Hs[k].d(), Dscr.d() + (2 * (k - 1) + 1) * 256 * 16, -kGramShift, int(a)});
+        jobs.push_back({G[k].d(), Dscr.d() + 2 * off, -kGramShift, int(a)});
+        jobs.push_back({Hs[k].d(), Dscr.d() + 2 * off + de, -kGramShift, int(a)});
+        off += de;
     }
     for (int b0 = 0; b0 < cnt; b0 += kPotrfBatchMax) {
         PotrfBatch pb{};
@@ -374,6 +399,7 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     for (size_t k = 1; k < d; ++k) {
         const size_t a = t.r[k], cols = t.cols_right(k);
         gemm(h, Hs[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
+        t.reduce(Hs[k].d(), a * a);
         da.G[nchk] = Hs[k].d();
         da.n[nchk] = int(a);
         ++nchk;
@@ -387,6 +413,10 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     XRS_HIP(hipStreamSynchronize(h->stream));
     bool ok = true;
     for (int i = 0; i < nchk * kSlices; ++i) ok = ok && (hd[i] <= 1e-13);   // NaN fails too
+    if (!ok && t.sharded()) {   // no sharded re-orthogonalisation sweep: report, cores untouched
+        for (size_t k = 0; k < d; ++k) t.release(C[k]);
+        return false;
+    }
     for (size_t k = 0; k < d; ++k) t.replace(k, C[k]);
     if (!ok) rl_sweep(t, max_ranks, eps, cX, d - 1);
     return true;
@@ -433,7 +463,7 @@ void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, 
 }
 
 double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
-           const double* const* Y) {
+           const double* const* Y, const TT* shard = nullptr) {
     size_t emax = 1, tmax = 1;
     for (size_t k = 0; k < d; ++k) {
         emax = std::max(emax, rx[k + 1] * ry[k + 1]);
@@ -450,6 +480,7 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
         gemm(h, T.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);
         // E' (a2 x b2) = T^T as ((b nk) x a2)^T * Y_k ((b nk) x b2)
         gemm(h, En, a2, b2, 1.0, T.d(), a2, true, b * nk, Y[k], b2, false);
+        if (shard) shard->reduce(En, a2 * b2);   // sum over all ranks' mode slices
         std::swap(E, En);
     }
     double* hs = static_cast<double*>(h->host_scratch);
@@ -518,6 +549,35 @@ int xrs_tt_round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** 
         XRS_REQUIRE(!canonicalized || core_position < d, "Illegal current core position");
         TT t{h, d, n, r, cores};
         round(t, canonicalized != 0, core_position, max_ranks, eps);
+    });
+}
+
+int xrs_tt_round_sharded(xrs_handle_t h, size_t d, const size_t* n_local, size_t* r, double** cores,
+                         const size_t* max_ranks, double eps, xrs_allreduce_fn allreduce, void* ctx, int* certified) {
+    return guarded([&] {
+        XRS_REQUIRE(h && certified && allreduce, "null argument");
+        XRS_REQUIRE(d >= 2 && n_local && r && cores, "null TT description");
+        XRS_REQUIRE(r[0] == 1 && r[d] == 1, "boundary ranks must be 1");
+        XRS_REQUIRE(eps < 1.0 && eps >= 0.0, "_eps must be smaller than one.");
+        for (size_t k = 0; k + 1 < d; ++k)
+            XRS_REQUIRE(max_ranks[k] > 0, "Trying to round a TTTensor to rank 0 is not possible.");
+        TT t{h, d, n_local, r, cores};
+        t.ar = allreduce;
+        t.ar_ctx = ctx;
+        *certified = round_chain(t, max_ranks, eps) ? 1 : 0;
+    });
+}
+
+int xrs_tt_dot_sharded(xrs_handle_t h, double* result, size_t d, const size_t* n_local, const size_t* rx,
+                       const double* const* X, const size_t* ry, const double* const* Y, xrs_allreduce_fn allreduce,
+                       void* ctx) {
+    return guarded([&] {
+        XRS_REQUIRE(h && result && allreduce, "null argument");
+        XRS_REQUIRE(d >= 1 && n_local && rx && ry && X && Y, "null TT description");
+        TT t{h, d, n_local, const_cast<size_t*>(rx), const_cast<double**>(X)};
+        t.ar = allreduce;
+        t.ar_ctx = ctx;
+        *result = dot(h, d, n_local, rx, X, ry, Y, &t);
     });
 }
 

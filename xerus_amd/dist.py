@@ -1,0 +1,141 @@
+"""Mode-sharded TT round and inner product across ranks.
+
+xerus is single-process (no MPI/NCCL anywhere in the reference), so this layer is new design, not a
+port. Layout: every rank holds, for every TT component k, a contiguous block of the mode index
+(``mode_partition``) -- the row blocks of the tall unfolding (r_k n_k) x r_{k+1}. Every quantity the
+round needs that sums over the mode index -- the left/right Gram chains, the orthogonality check, the
+<x,y> zipper environments -- is a local GEMM followed by one all-reduce of an r x r matrix
+(``xrs_allreduce_fn``, bound here to torch.distributed: RCCL over xGMI with the "nccl" backend, or
+gloo with host staging); the per-core transforms are purely local. No data-path all-gather is needed.
+
+The product path is the HIP library (xrs_tt_round_sharded / xrs_tt_dot_sharded); the helpers below
+only partition, gather and move bytes.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Callable, Sequence
+
+import numpy as np
+
+from . import capi
+
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+
+
+def mode_partition(n: int, world: int, rank: int) -> tuple[int, int]:
+    """Balanced contiguous block [start, start+count) of the mode index 0..n-1 owned by `rank`."""
+    base, extra = divmod(n, world)
+    start = rank * base + min(rank, extra)
+    return start, base + (1 if rank < extra else 0)
+
+
+def shard_cores(cores: Sequence[np.ndarray], world: int, rank: int) -> list[np.ndarray]:
+    """This rank's mode slices of full cores (r_k, n_k, r_{k+1})."""
+    out = []
+    for c in cores:
+        s, m = mode_partition(c.shape[1], world, rank)
+        out.append(np.ascontiguousarray(c[:, s:s + m, :]))
+    return out
+
+
+def unshard_cores(parts: Sequence[Sequence[np.ndarray]]) -> list[np.ndarray]:
+    """Reassemble full cores from every rank's slices (parts[rank][k]), in rank order."""
+    d = len(parts[0])
+    return [np.concatenate([p[k] for p in parts], axis=1) for k in range(d)]
+
+
+class _CudaArray:
+    """__cuda_array_interface__ view of raw device memory (float64)."""
+
+    def __init__(self, ptr: int, count: int):
+        self.__cuda_array_interface__ = {"shape": (count,), "typestr": "<f8", "data": (ptr, False), "version": 3}
+
+
+class TorchAllReduce:
+    """xrs_allreduce_fn backed by torch.distributed (sum, in place on the device buffer).
+
+    nccl (= RCCL on ROCm) reduces the device buffer directly; gloo reduces a host copy."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.torch, self.dist, self.group = torch, dist, group
+        self.device_native = dist.get_backend(group) == "nccl"
+        self.calls = 0
+        self.bytes = 0
+
+        def _cb(_ctx, ptr, count):
+            try:
+                t = self.torch.as_tensor(_CudaArray(int(ptr), int(count)), device="cuda")
+                if self.device_native:
+                    self.dist.all_reduce(t, group=self.group)
+                    self.torch.cuda.synchronize()
+                else:
+                    h = t.cpu()
+                    self.dist.all_reduce(h, group=self.group)
+                    t.copy_(h)
+                    self.torch.cuda.synchronize()
+                self.calls += 1
+                self.bytes += 8 * int(count)
+                return 0
+            except Exception:   # reported to the C side as a failed collective
+                return 1
+
+        self.fn = ALLREDUCE_FN(_cb)   # keep a reference: the C side only holds the pointer
+
+    @property
+    def c_fn(self):
+        return C.cast(self.fn, C.c_void_p)
+
+
+class ShardedTT:
+    """This rank's mode slices of a TT (capi.TTDevice over the local slices) + the global mode sizes."""
+
+    def __init__(self, handle: capi.Handle, local: capi.TTDevice, dims: Sequence[int], world: int, rank: int):
+        self.handle, self.local, self.dims, self.world, self.rank = handle, local, list(dims), world, rank
+
+    @classmethod
+    def from_full_cores(cls, handle: capi.Handle, cores, world: int, rank: int) -> "ShardedTT":
+        dims = [c.shape[1] for c in cores]
+        return cls(handle, capi.TTDevice.from_cores(handle, shard_cores(cores, world, rank)), dims, world, rank)
+
+    @property
+    def ranks(self):
+        return self.local.ranks
+
+    def round(self, max_ranks, comm: TorchAllReduce, eps: float = 8 * np.finfo(float).eps) -> bool:
+        """Certified sharded round in place; returns False (cores untouched) if the certificate fails."""
+        t = self.local
+        d = t.order
+        if isinstance(max_ranks, (int, np.integer)):
+            max_ranks = [int(max_ranks)] * (d - 1)
+        n, r, cores = t._arrays()
+        mr = capi._arr(list(max_ranks) + [1])
+        cert = C.c_int(0)
+        st = self.handle.lib.xrs_tt_round_sharded(self.handle.h, d, n, r, cores, mr, eps, comm.c_fn, None,
+                                                  C.byref(cert))
+        t._writeback(r, cores)
+        capi._check("xrs_tt_round_sharded", st)
+        if cert.value:
+            t.canonicalized, t.core_position = True, 0
+        return bool(cert.value)
+
+    def dot(self, other: "ShardedTT", comm: TorchAllReduce) -> float:
+        x, y = self.local, other.local
+        d = x.order
+        out = C.c_double()
+        xc = (capi._DP * d)(*[capi._DP(p) for p in x.ptrs])
+        yc = (capi._DP * d)(*[capi._DP(p) for p in y.ptrs])
+        capi._check("xrs_tt_dot_sharded",
+                    self.handle.lib.xrs_tt_dot_sharded(self.handle.h, C.byref(out), d, capi._arr(x.dims),
+                                                       capi._arr(x.r), xc, capi._arr(y.r), yc, comm.c_fn, None))
+        return out.value
+
+    def gather(self, all_gather_object: Callable) -> list[np.ndarray]:
+        """Full cores on every rank (all_gather_object: torch.distributed.all_gather_object-like)."""
+        mine = self.local.cores()
+        parts = [None] * self.world
+        all_gather_object(parts, mine)
+        return unshard_cores(parts)
