@@ -1,17 +1,20 @@
 """Benchmark of the MI355X TT hot path: "GFLOP/s on TT contraction + TT-round sweep time, order-10 rank-256".
 
-One step = one TT inner product <x, y> (core-chain contraction) + one x.round(256) sweep on synthetic
-random TTs of order 10, mode size 20, rank 256 (BASELINE.json north star; TTTensor::random semantics:
-N(0,1) cores, then move_core(0)). Inputs are resident in HBM before the timed region; the round result
-is canonical at core 0 with the same ranks, so every step repeats exactly the same work.
+Headline step = one TT inner product <x, y> (core-chain contraction) + one x.round(256) on synthetic
+random TTs of order 10, mode size 20, rank 256 (BASELINE.json north star). Inputs follow
+TTTensor::random (ttNetwork.h:129-157): N(0,1) cores drawn by the product's own libstdc++ mt19937_64 +
+normal_distribution (the reference's generator, xerus_amd.xerus.TTTensor.random_raw), then move_core(0)
+on the GPU. They are resident in HBM before the timed region; round() keeps the tensor, the ranks and
+the canonical form, so every step repeats the same work.
 
-value = algorithmic GFLOP of the step / wall time (SURVEY §8(d) formulas, not hardware counters):
+value = algorithmic GFLOP of the step / wall time (SURVEY 8(d) formulas, not hardware counters):
   <x,y>  : sum_k 2 a_x a_y n b_x + 2 a_y n b_x b_y           (zipper)
   round  : sum_edges 6 a n b^2 + 6 b^2 n' c + 22 b^3         (standard two-sweep TT rounding)
-Multi-GPU: one process per GPU, every rank rounds/contracts its own TT pair (replicas, weak scaling,
-no data-path collective); value = all ranks' flops / max-over-ranks time.
+Multi-GPU: one process per GPU; the headline is replicas (every rank its own TT pair, weak scaling, no
+data-path collective). The "cfg5" object adds BASELINE configs[4]: order-16 rank-512 round() sharded
+over all ranks by mode slices (xerus_amd.dist; one r x r all-reduce per edge over RCCL), strong scaling.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu] [--no-cfg5]
 """
 import argparse
 import json
@@ -25,10 +28,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # gfx950 dense fp64 matrix peak (MI355X spec)
-HBM_PEAK_GBS = 8000.0
+SEED = 0xBAADF00D               # src/xerus/test/test.cpp:105
 
 
 def tt_ranks(d, n, r):
+    """reduce_to_maximal_ranks (ttNetwork.cpp:370-402) of a uniform rank r, with the boundary 1s."""
     ranks = [r] * (d - 1)
     cur = 1
     for i in range(d - 1):
@@ -60,6 +64,70 @@ def flops_round(dims, r):
     return f
 
 
+def random_cores(xe, dims, ranks, seed):
+    """TTTensor::random_raw through the product's C++ API: the reference's RNG stream, cores (r, n, r')."""
+    xe.seed(seed)
+    tt = xe.TTTensor.random_raw(list(dims), list(ranks[1:-1]))
+    return [np.ascontiguousarray(tt.get_component(k).to_ndarray()) for k in range(len(dims))]
+
+
+def load_traffic():
+    """HBM bytes per k_gemm_f64 launch from the committed rocprofv3 PMC pass of this bench (or None)."""
+    p = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def bench_cfg5(h, xe, world, rank, dist, sync, steps, warmup):
+    """BASELINE configs[4]: TTTensor order 16, n = 20, rank 512, round(512) sharded over all ranks."""
+    from xerus_amd import dist as xd
+
+    d, n, r = 16, 20, 512
+    dims = [n] * d
+    ranks = tt_ranks(d, n, r)
+    cores = random_cores(xe, dims, ranks, SEED + 5)          # identical on every rank
+    st = xd.ShardedTT.from_full_cores(h, cores, world, rank)
+    del cores
+    comm = xd.TorchAllReduce()
+    cert = st.round(r, comm)                                  # first call canonicalises (right-canonical)
+    for _ in range(max(0, warmup - 1)):
+        cert = st.round(r, comm) and cert
+    calls0 = comm.calls
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cert = st.round(r, comm) and cert
+    h.synchronize()
+    sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    f = flops_round(dims, ranks)
+    ms = elapsed / steps * 1e3
+    out = {
+        "workload": f"TT order-{d} n={n} rank-{r}: round({r}) sharded by mode slices over {world} rank(s)",
+        "ms_per_round": round(ms, 3),
+        "gflop_per_round": round(f / 1e9, 2),
+        "tflops": round(f / (ms * 1e-3) / 1e12, 3),
+        "scaling": "strong",
+        "certified": bool(cert),
+        "ranks_unchanged": st.ranks == ranks[1:-1],
+        "allreduce_per_round": (comm.calls - calls0) / steps,
+        "steps": steps,
+    }
+    st.local.free()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,7 +137,8 @@ def main():
     ap.add_argument("--mode", type=int, default=20)
     ap.add_argument("--rank", type=int, default=256)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-steps", type=int, default=8)
+    ap.add_argument("--no-cfg5", action="store_true", help="skip the sharded order-16 rank-512 round")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -86,19 +155,18 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from oracle import xerus_ref as ref   # input generator (libstdc++ RNG restatement) + CPU baseline leg
+    import xerus_amd.xerus as xe
     from xerus_amd import capi
 
+    xe.set_device(local)
     h = capi.Handle(local)
     d, n, r = args.order, args.mode, args.rank
     dims = [n] * d
     ranks = tt_ranks(d, n, r)
-    rng = ref.Rng(ref.Rng.SEED + rank)
-    # synthetic TTTensor::random inputs: raw N(0,1) cores uploaded, then move_core(0) ON THE GPU
-    xr = ref.TT.random_raw(dims, ranks[1:-1], rng)
-    yr = ref.TT.random_raw(dims, ranks[1:-1], rng)
-    x = capi.TTDevice.from_cores(h, xr.cores)
-    y = capi.TTDevice.from_cores(h, yr.cores)
+    xc = random_cores(xe, dims, ranks, SEED + 2 * rank)
+    yc = random_cores(xe, dims, ranks, SEED + 2 * rank + 1)
+    x = capi.TTDevice.from_cores(h, xc)
+    y = capi.TTDevice.from_cores(h, yc)
     x.move_core(0)
     y.move_core(0)
     assert x.r == ranks and y.r == ranks, (x.r, ranks)
@@ -145,9 +213,21 @@ def main():
 
     ms_step = elapsed / args.steps * 1e3
     value = world * f_step * args.steps / elapsed / 1e9
+    assert x.r == ranks
+
+    cfg5 = None
+    if not args.no_cfg5:
+        x.free()
+        y.free()
+        try:
+            cfg5 = bench_cfg5(h, xe, world, rank, dist, barrier, steps=3, warmup=1)
+        except Exception as e:   # reported, never fatal for the headline line
+            cfg5 = {"error": f"{type(e).__name__}: {e}"}
 
     if rank == 0:
+        launches = max(1, prof["launches"])
         gemm_tflops = prof["flops"] / (prof["ms"] * 1e-3) / 1e12 if prof["ms"] > 0 else 0.0
+        traffic = load_traffic()
         roofline = {
             "bound": "mfma",
             "kernel": "k_gemm_f64 (all GEMM launches of the step, fp64 MFMA 16x16x4)",
@@ -155,27 +235,32 @@ def main():
             "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(gemm_tflops / FP64_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None,
+            "traffic": traffic.get("hbm_bytes_per_launch") if traffic else None,
+            "traffic_source": traffic.get("source") if traffic else None,
             "launches_per_step": prof["launches"] / args.steps,
-            "avg_launch_us": prof["ms"] / max(1, prof["launches"]) * 1e3,
-            "algorithmic_flops_per_launch": prof["flops"] / max(1, prof["launches"]),
+            "avg_launch_us": round(prof["ms"] / launches * 1e3, 3),
+            "algorithmic_flops_per_launch": prof["flops"] / launches,
+            "algorithmic_bytes_per_launch": prof["bytes"] / launches,
         }
         cpu = None
         if not args.no_cpu:
+            # CPU baseline leg: the oracle (numpy/scipy-LAPACK restatement of the reference algorithm)
+            from oracle import xerus_ref as ref
+
             try:
                 from threadpoolctl import threadpool_limits
             except ImportError:
                 threadpool_limits = None
-            xc, yc = xr.copy(), yr.copy()
-            xc.move_core(0)
-            yc.move_core(0)
+            xo, yo = ref.TT([c.copy() for c in xc]), ref.TT([c.copy() for c in yc])
+            xo.move_core(0)
+            yo.move_core(0)
             ctx = threadpool_limits(limits=1) if threadpool_limits else None
             if ctx:
                 ctx.__enter__()
             t_c = time.perf_counter()
             for _ in range(args.cpu_steps):
-                ref.dot(xc, yc)
-                xc.round(r)
+                ref.dot(xo, yo)
+                xo.round(r)
             t_c = time.perf_counter() - t_c
             if ctx:
                 ctx.__exit__(None, None, None)
@@ -185,8 +270,8 @@ def main():
                 "cores": 1,
                 "kind": "port",
                 "sample": f"{args.cpu_steps} full steps (<x,y> + round({r})) of the same order-{d} n={n} r={r} "
-                          f"workload, numpy/scipy-LAPACK restatement of the reference (dgeqp3/dorgqr/dgesdd/dgemm), "
-                          f"1 BLAS thread, {t_c:.2f} s",
+                          f"workload and inputs, numpy/scipy-LAPACK restatement of the reference "
+                          f"(dgeqp3/dorgqr/dgesdd/dgemm call sequence), 1 BLAS thread, {t_c:.2f} s",
                 "ms_per_step": round(t_c / args.cpu_steps * 1e3, 2),
             }
         out = {
@@ -201,8 +286,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (TTTensor::random semantics: N(0,1) cores via mt19937_64 seeded 0xBAADF00D + rank, "
-                    "move_core(0) on the GPU)",
+            "data": "synthetic (TTTensor::random semantics: N(0,1) cores from the product's libstdc++ mt19937_64 "
+                    "seeded 0xBAADF00D + 2 rank (+1 for y), move_core(0) on the GPU)",
             "config": {
                 "workload": f"TT order-{d} n={n} rank-{r}: <x,y> + x.round({r}) per step",
                 "order": d, "mode_size": n, "rank": r, "ranks": ranks,
@@ -213,8 +298,9 @@ def main():
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cfg5": cfg5,
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
