@@ -1,6 +1,8 @@
 // Handle, stream, caching allocator, profiler and the runtime part of the C-ABI.
 #include "runtime.hpp"
 
+#include <algorithm>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -121,14 +123,20 @@ extern "C" {
 const char* xrs_last_error(void) { return g_last_error.c_str(); }
 const char* xrs_version(void) { return "xerus_amd 0.1 (gfx950)"; }
 
-StreamFork::StreamFork(xrs_handle_t h) : h_(h), main_stream_(h->stream), main_pool_(h->pool) {
+StreamFork::StreamFork(xrs_handle_t h, int sides)
+    : h_(h), sides_(std::max(1, std::min(sides, int(xrs_handle_s::kSides)))), main_stream_(h->stream), main_pool_(h->pool) {
     XRS_HIP(hipEventRecord(h_->ev_fork, main_stream_));
-    XRS_HIP(hipStreamWaitEvent(h_->side_stream, h_->ev_fork, 0));
+    for (int i = 0; i < sides_; ++i) XRS_HIP(hipStreamWaitEvent(h_->side_stream[i], h_->ev_fork, 0));
 }
 
-void StreamFork::side() {
-    h_->stream = h_->side_stream;
-    h_->pool = h_->side_pool;
+void StreamFork::side(int i) {
+    h_->stream = h_->side_stream[i];
+    h_->pool = h_->side_pool[i];
+}
+
+void StreamFork::lane(int i) {
+    if (i <= 0) main();
+    else side((i - 1) % sides_);
 }
 
 void StreamFork::main() {
@@ -140,8 +148,10 @@ void StreamFork::join() {
     if (joined_) return;
     joined_ = true;
     main();
-    XRS_HIP(hipEventRecord(h_->ev_join, h_->side_stream));
-    XRS_HIP(hipStreamWaitEvent(main_stream_, h_->ev_join, 0));
+    for (int i = 0; i < sides_; ++i) {
+        XRS_HIP(hipEventRecord(h_->ev_join[i], h_->side_stream[i]));
+        XRS_HIP(hipStreamWaitEvent(main_stream_, h_->ev_join[i], 0));
+    }
 }
 
 StreamFork::~StreamFork() {
@@ -163,10 +173,12 @@ int xrs_create(xrs_handle_t* handle, int device) {
         XRS_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
         h->stream = h->own_stream;
         h->pool = new Pool(device);
-        XRS_HIP(hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
-        h->side_pool = new Pool(device);
+        for (int i = 0; i < xrs_handle_s::kSides; ++i) {
+            XRS_HIP(hipStreamCreateWithFlags(&h->side_stream[i], hipStreamNonBlocking));
+            h->side_pool[i] = new Pool(device);
+            XRS_HIP(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
+        }
         XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-        XRS_HIP(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
         *handle = h;
@@ -183,12 +195,15 @@ int xrs_destroy(xrs_handle_t h) {
             (void)hipEventDestroy(r.stop);
         }
         for (auto e : h->event_cache) (void)hipEventDestroy(e);
-        if (h->side_stream) (void)hipStreamSynchronize(h->side_stream);
+        for (auto s : h->side_stream)
+            if (s) (void)hipStreamSynchronize(s);
         delete h->pool;
-        delete h->side_pool;
-        if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
+        for (int i = 0; i < xrs_handle_s::kSides; ++i) {
+            delete h->side_pool[i];
+            if (h->side_stream[i]) (void)hipStreamDestroy(h->side_stream[i]);
+            if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
+        }
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-        if (h->ev_join) (void)hipEventDestroy(h->ev_join);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);

@@ -88,10 +88,11 @@ struct xrs_handle_s {
     void* host_scratch = nullptr;
     // device scratch for reductions / statuses (64 KiB)
     void* dev_scratch = nullptr;
-    // side stream (+ its own stream-ordered pool) for independent work forked from `stream`
-    hipStream_t side_stream = nullptr;
-    xrs::Pool* side_pool = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    // side streams (each with its own stream-ordered pool) for independent work forked from `stream`
+    static constexpr int kSides = 3;
+    hipStream_t side_stream[kSides] = {};
+    xrs::Pool* side_pool[kSides] = {};
+    hipEvent_t ev_fork = nullptr, ev_join[kSides] = {};
     // profiler
     uint32_t prof_mask = 0;
     std::vector<xrs::ProfRecord> prof;
@@ -143,13 +144,16 @@ void check_launch(const char* what);
 // buffers shared across the fork must be allocated before it and released after join().
 class StreamFork {
    public:
-    explicit StreamFork(xrs_handle_t h);
+    explicit StreamFork(xrs_handle_t h, int sides = 1);
     ~StreamFork();
-    void side();   // switch to the side stream (after the fork point)
-    void main();   // switch back
-    void join();   // main stream waits for the side stream's work
+    void side(int i = 0);   // switch to side stream i < sides (after the fork point)
+    void lane(int i);       // 0 = main stream, 1..sides = side stream i-1 (round-robin helper)
+    void main();            // switch back
+    void join();            // main stream waits for every side stream's work
+    int lanes() const { return sides_ + 1; }
    private:
     xrs_handle_t h_;
+    int sides_;
     hipStream_t main_stream_;
     Pool* main_pool_;
     bool joined_ = false;

@@ -389,20 +389,28 @@ bool chain_pass(TT& t, bool certify, std::vector<double*>& C) {
                              hs[i]);
             return false;
         }
+    // the d transforms are independent: spread them over the main and side streams (buffers they share
+    // with the rest of the round are allocated before the fork and released after the join)
     C.assign(d, nullptr);
-    size_t wmax = 1;
-    for (size_t k = 0; k < d; ++k) wmax = std::max(wmax, t.size(k));
-    DevBuf W(h, wmax * 8);
+    std::vector<DevBuf> W(d);
     for (size_t k = 0; k < d; ++k) {
-        const size_t a = t.r[k], b = t.r[k + 1], rows = t.rows_left(k), cols = t.cols_right(k);
         C[k] = t.alloc(t.size(k));
-        const double* src = t.core[k];
-        if (k + 1 < d) {   // M_k (I (x) L_{k+1}): (r_k n_k) x r_{k+1} times r_{k+1} x r_{k+1}
-            gemm(h, k == 0 ? C[k] : W.d(), rows, b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);
-            src = W.d();
+        if (k > 0 && k + 1 < d) W[k] = DevBuf(h, t.size(k) * 8);
+    }
+    {
+        StreamFork fork(h, xrs_handle_s::kSides);
+        for (size_t k = 0; k < d; ++k) {
+            fork.lane(int(k % size_t(fork.lanes())));
+            const size_t a = t.r[k], b = t.r[k + 1], rows = t.rows_left(k), cols = t.cols_right(k);
+            const double* src = t.core[k];
+            if (k + 1 < d) {   // M_k (I (x) L_{k+1}): (r_k n_k) x r_{k+1} times r_{k+1} x r_{k+1}
+                gemm(h, k == 0 ? C[k] : W[k].d(), rows, b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);
+                src = W[k].d();
+            }
+            if (k > 0) trsm(h, true, H[k].d(), dinv[k], int(a), src, cols, C[k], cols, int(cols));
+            else if (k + 1 == d) XRS_HIP(hipMemcpyAsync(C[k], src, t.size(k) * 8, hipMemcpyDeviceToDevice, h->stream));
         }
-        if (k > 0) trsm(h, true, H[k].d(), dinv[k], int(a), src, cols, C[k], cols, int(cols));
-        else if (k + 1 == d) XRS_HIP(hipMemcpyAsync(C[k], src, t.size(k) * 8, hipMemcpyDeviceToDevice, h->stream));
+        fork.join();
     }
     return true;
 }
@@ -415,13 +423,25 @@ double chain_check(TT& t, const std::vector<double*>& C) {
     DevIdArgs da{};
     DevBuf dev(h, d * 16 * 8 + 64);
     int nchk = 0;
+    for (size_t k = 1; k < d; ++k) Gr[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
+    if (t.sharded()) {   // the all-reduce hook synchronises the stream: stay on it
+        for (size_t k = 1; k < d; ++k) {
+            const size_t a = t.r[k], cols = t.cols_right(k);
+            gemm(h, Gr[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
+            t.reduce(Gr[k].d(), a * a);
+        }
+    } else {
+        StreamFork fork(h, xrs_handle_s::kSides);
+        for (size_t k = 1; k < d; ++k) {
+            fork.lane(int(k % size_t(fork.lanes())));
+            const size_t a = t.r[k], cols = t.cols_right(k);
+            gemm(h, Gr[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
+        }
+        fork.join();
+    }
     for (size_t k = 1; k < d; ++k) {
-        const size_t a = t.r[k], cols = t.cols_right(k);
-        Gr[k] = DevBuf(h, a * a * 8);
-        gemm(h, Gr[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
-        t.reduce(Gr[k].d(), a * a);
         da.G[nchk] = Gr[k].d();
-        da.n[nchk] = int(a);
+        da.n[nchk] = int(t.r[k]);
         ++nchk;
     }
     da.out = dev.d();
