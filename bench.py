@@ -10,6 +10,9 @@ the canonical form, so every step repeats the same work.
 value = algorithmic GFLOP of the step / wall time (SURVEY 8(d) formulas, not hardware counters):
   <x,y>  : sum_k 2 a_x a_y n b_x + 2 a_y n b_x b_y           (zipper)
   round  : sum_edges 6 a n b^2 + 6 b^2 n' c + 22 b^3         (standard two-sweep TT rounding)
+roofline: a second pass of the same K steps with a HIP event pair around every GEMM launch gives the
+average GEMM launch duration (event packets add GPU time between kernels, so that pass is not the
+headline timing; its ms/step is reported as roofline.events_pass_ms_per_step).
 Multi-GPU: one process per GPU; the headline is replicas (every rank its own TT pair, weak scaling, no
 data-path collective). The "cfg5" object adds BASELINE configs[4]: order-16 rank-512 round() sharded
 over all ranks by mode slices (xerus_amd.dist; one r x r all-reduce per edge over RCCL), strong scaling.
@@ -197,13 +200,23 @@ def main():
         torch.cuda.synchronize()
 
     barrier()
-    h.prof_begin(capi.KFAM_GEMM)
     timing = {"dot": 0.0, "round": 0.0}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timing)
     barrier()
     elapsed = time.perf_counter() - t0
+
+    # Roofline pass: the same K steps again with a HIP event pair around every GEMM launch (on the stream
+    # each launch goes to). The event packets add GPU-side work between kernels, so this pass is kept out
+    # of the headline timing; its wall time is reported beside it.
+    barrier()
+    h.prof_begin(capi.KFAM_GEMM)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed_ev = time.perf_counter() - t0
     prof = h.prof_end()
 
     if dist is not None:
@@ -239,6 +252,7 @@ def main():
             "traffic_source": traffic.get("source") if traffic else None,
             "launches_per_step": prof["launches"] / args.steps,
             "avg_launch_us": round(prof["ms"] / launches * 1e3, 3),
+            "events_pass_ms_per_step": round(elapsed_ev / args.steps * 1e3, 4),
             "algorithmic_flops_per_launch": prof["flops"] / launches,
             "algorithmic_bytes_per_launch": prof["bytes"] / launches,
         }

@@ -8,9 +8,9 @@
 //   C/D (f64 only): col = l&15, row = (l>>4) + 4*reg  (cdna_hip_programming.md §3).
 // LDS row stride S = B? + 17 doubles (odd): transposed ds_write_b64 of the k-contiguous operands is
 // conflict-free in each 16-lane group, and the k/k+1 fragment rows of ds_read_b64 overlap in one bank.
-// Split-K (grid.z) writes fp64 partial slabs that a second kernel reduces in fixed order
-// (bitwise reproducible), used when the M x N tile grid alone cannot fill 256 CUs (TT shapes:
-// 256 x 256 outputs with K = n*r up to 10240).
+// Split-K (grid.z) writes fp64 partial slabs that the last-arriving slice of each tile sums in fixed
+// order (bitwise reproducible) inside the same launch, used when the M x N tile grid alone cannot fill
+// 256 CUs (TT shapes: 256 x 256 outputs with K = n*r up to 10240).
 #include <algorithm>
 #include <type_traits>
 #include <utility>
@@ -27,7 +27,7 @@ template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, b
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64, (WGM * WGN * WGK * 64 * 2 <= 1024) ? 2 : 1)
 k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ B, size_t ldb,
            double* __restrict__ C, int M, int N, int K, int kps, double alpha, double* __restrict__ slab,
-           int tiles_m, int xcd_group) {
+           int tiles_m, int xcd_group, int* __restrict__ tickets) {
     constexpr int NT = WGM * WGN * WGK * 64;   // WGK wave groups split every K-step's MFMA k-substeps
     // LDS rows of BM / BN doubles, XOR-swizzled per k row: element (k, m) at k*SA + (m ^ swz(k)) with
     // swz(k) = 16*(k&1) + (k>>1). Fragment reads (lanes: 16 m x rows k, k+1) hit 32 distinct bank pairs
@@ -220,7 +220,8 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
                         red[((((kg - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane] = acc[i][j][r];
         }
         __syncthreads();
-        if (kg > 0) return;
+        if (kg > 0 && tickets == nullptr) return;   // (with tickets every wave stays for the barriers below)
+        if (kg == 0)
 #pragma unroll
         for (int g = 1; g < WGK; ++g)
 #pragma unroll
@@ -233,9 +234,45 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
     }
     // ---- epilogue
     const bool to_slab = slab != nullptr;
-    double* out = to_slab ? slab + size_t(blockIdx.z) * size_t(M) * size_t(N) : C;
+    const size_t MN = size_t(M) * size_t(N);
+    double* out = to_slab ? slab + size_t(blockIdx.z) * MN : C;
     const double scale = to_slab ? 1.0 : alpha;
     const int lc = lane & 15, lg = lane >> 4;
+    if (kg == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = n0 + wn + j * 16 + lc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wm + i * 16 + lg + 4 * r;
+                    if (row < M && col < N) {
+                        if (tickets != nullptr)   // write-through (sc1): visible to any XCD without a release fence
+                            __hip_atomic_store(&out[size_t(row) * N + col], acc[i][j][r], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else
+                            out[size_t(row) * N + col] = scale * acc[i][j][r];
+                    }
+                }
+            }
+    }
+    if (tickets == nullptr) return;
+    // ---- in-launch split-K combine (cdna_hip_programming.md §5 projection-GEMM item 2, sc1 form): every
+    // slice stores its slab write-through (sc1, above), drains its stores and draws a ticket; the slice
+    // that draws splits-1 reads the other slabs with sc1 loads (no fences anywhere) and sums them in
+    // slice order 0..splits-1 -- the order of k_splitk_reduce, so both forms are bitwise identical.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    double* flag = &As[0][0];   // the one LDS array (no second __shared__ object, see the guide's trap 4a)
+    if (tid == 0) {
+        const int t = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = (t == int(gridDim.z) - 1);
+        if (last) __hip_atomic_store(&tickets[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = last ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (flag[0] == 0.0 || kg != 0) return;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -244,7 +281,15 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = m0 + wm + i * 16 + lg + 4 * r;
-                if (row < M && col < N) out[size_t(row) * N + col] = scale * acc[i][j][r];
+                if (row < M && col < N) {
+                    const size_t o = size_t(row) * N + col;
+                    double sum = 0.0;
+                    for (int z = 0; z < int(gridDim.z); ++z)
+                        sum += (z == int(blockIdx.z)) ? acc[i][j][r]
+                                                      : __hip_atomic_load(&slab[size_t(z) * MN + o], __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    C[o] = alpha * sum;
+                }
             }
         }
 }
@@ -261,19 +306,20 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(double* __restrict__ C, c
 
 template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD>
 static void launch_tiles(xrs_handle_t h, const double* A, size_t lda, bool ta, const double* B, size_t ldb, bool tb,
-                         double* C, int M, int N, int K, int splits, int kps, double alpha, double* slab) {
+                         double* C, int M, int N, int K, int splits, int kps, double alpha, double* slab, int* tickets) {
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     dim3 grid(unsigned(tiles_m * tiles_n), 1, unsigned(splits));
     // group by the larger operand's panels (B: K x N, A: M x K) when the tile grid allows a bijection
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
-    if (std::getenv("XRS_GEMM_NOXCD")) xg = 0;
+    static const bool noxcd = std::getenv("XRS_GEMM_NOXCD") != nullptr;
+    if (noxcd) xg = 0;
     KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(M) * double(N) * double(K),
                       8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GEMM_LAUNCH(TA_, TB_)                                                                             \
     hipLaunchKernelGGL((k_gemm_f64<BM, BN, GBK, WGM, WGN, WGK, PD, TA_, TB_>), grid, dim3(WGM * WGN * WGK * 64), 0, h->stream, A, lda, B, ldb, C, M, N, K, \
-                       kps, alpha, slab, tiles_m, xg)
+                       kps, alpha, slab, tiles_m, xg, tickets)
     if (!ta && !tb) XRS_GEMM_LAUNCH(false, false);
     else if (!ta && tb) XRS_GEMM_LAUNCH(false, true);
     else if (ta && !tb) XRS_GEMM_LAUNCH(true, false);
@@ -325,16 +371,24 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
     splits = (K + kps - 1) / kps;
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(splits) * M * N * sizeof(double));
+    // one-launch split-K when the tile grid fits the stream's ticket array (XRS_GEMM_SPLITK2=1: old
+    // two-kernel form, for A/B timing)
+    static const bool two_kernel = std::getenv("XRS_GEMM_SPLITK2") != nullptr;
+    // The last arriver reads splits x BM x BN doubles serially: worth it for small tiles only (the guide's
+    // "a few tens of KB" per tile; 128x128 tiles at 2 splits measured 70 us slower than the reduce kernel).
+    const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= 65536;
+    int* tickets = (splits > 1 && !two_kernel && small_slab && ntiles(bms[var], bns[var]) <= xrs_handle_s::kTicketCap)
+                       ? h->tickets : nullptr;
     switch (var) {
-        case 1: launch_tiles<128, 128, 16, 2, 4, 1, 2>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
-        case 2: launch_tiles<64, 64, 16, 2, 4, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
-        case 3: launch_tiles<64, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
-        case 5: launch_tiles<64, 32, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
-        case 6: launch_tiles<64, 64, 32, 2, 2, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
-        case 7: launch_tiles<64, 64, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
-        default: launch_tiles<32, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d()); break;
+        case 1: launch_tiles<128, 128, 16, 2, 4, 1, 2>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        case 2: launch_tiles<64, 64, 16, 2, 4, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        case 3: launch_tiles<64, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        case 5: launch_tiles<64, 32, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        case 6: launch_tiles<64, 64, 32, 2, 2, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        case 7: launch_tiles<64, 64, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        default: launch_tiles<32, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
     }
-    if (splits > 1) {
+    if (splits > 1 && tickets == nullptr) {
         const size_t MN = size_t(M) * N;
         const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
         KernelTimer timer(h, XRS_KFAM_ELEMWISE, double(MN) * splits, 8.0 * double(MN) * (splits + 1));

@@ -124,7 +124,8 @@ const char* xrs_last_error(void) { return g_last_error.c_str(); }
 const char* xrs_version(void) { return "xerus_amd 0.1 (gfx950)"; }
 
 StreamFork::StreamFork(xrs_handle_t h, int sides)
-    : h_(h), sides_(std::max(1, std::min(sides, int(xrs_handle_s::kSides)))), main_stream_(h->stream), main_pool_(h->pool) {
+    : h_(h), sides_(std::max(1, std::min(sides, int(xrs_handle_s::kSides)))), main_stream_(h->stream), main_pool_(h->pool),
+      main_tickets_(h->tickets) {
     XRS_HIP(hipEventRecord(h_->ev_fork, main_stream_));
     for (int i = 0; i < sides_; ++i) XRS_HIP(hipStreamWaitEvent(h_->side_stream[i], h_->ev_fork, 0));
 }
@@ -132,6 +133,7 @@ StreamFork::StreamFork(xrs_handle_t h, int sides)
 void StreamFork::side(int i) {
     h_->stream = h_->side_stream[i];
     h_->pool = h_->side_pool[i];
+    h_->tickets = h_->side_tickets[i];
 }
 
 void StreamFork::lane(int i) {
@@ -142,6 +144,7 @@ void StreamFork::lane(int i) {
 void StreamFork::main() {
     h_->stream = main_stream_;
     h_->pool = main_pool_;
+    h_->tickets = main_tickets_;
 }
 
 void StreamFork::join() {
@@ -181,6 +184,12 @@ int xrs_create(xrs_handle_t* handle, int device) {
         XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
+        const size_t tbytes = size_t(1 + xrs_handle_s::kSides) * xrs_handle_s::kTicketCap * sizeof(int);
+        XRS_HIP(hipMalloc(&h->ticket_base, tbytes));
+        XRS_HIP(hipMemset(h->ticket_base, 0, tbytes));
+        h->tickets = h->ticket_base;
+        for (int i = 0; i < xrs_handle_s::kSides; ++i)
+            h->side_tickets[i] = h->ticket_base + size_t(1 + i) * xrs_handle_s::kTicketCap;
         *handle = h;
     });
 }
@@ -206,6 +215,7 @@ int xrs_destroy(xrs_handle_t h) {
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
+        (void)hipFree(h->ticket_base);
         if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
         delete h;
     });
@@ -214,7 +224,10 @@ int xrs_destroy(xrs_handle_t h) {
 int xrs_set_stream(xrs_handle_t h, void* s) {
     return guarded([&] {
         XRS_REQUIRE(h, "null handle");
-        h->stream = s ? static_cast<hipStream_t>(s) : h->own_stream;
+        hipStream_t next = s ? static_cast<hipStream_t>(s) : h->own_stream;
+        // the pool and the split-K tickets are stream-ordered: drain the old stream before switching
+        if (next != h->stream) XRS_HIP(hipStreamSynchronize(h->stream));
+        h->stream = next;
     });
 }
 

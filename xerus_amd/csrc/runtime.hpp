@@ -93,6 +93,12 @@ struct xrs_handle_s {
     hipStream_t side_stream[kSides] = {};
     xrs::Pool* side_pool[kSides] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kSides] = {};
+    // split-K arrival tickets (zero between launches; the last arriving slice resets its word), one
+    // array per stream so concurrent launches never share a word; `tickets` follows `stream`
+    static constexpr int kTicketCap = 4096;
+    int* ticket_base = nullptr;
+    int* tickets = nullptr;
+    int* side_tickets[kSides] = {};
     // profiler
     uint32_t prof_mask = 0;
     std::vector<xrs::ProfRecord> prof;
@@ -156,6 +162,7 @@ class StreamFork {
     int sides_;
     hipStream_t main_stream_;
     Pool* main_pool_;
+    int* main_tickets_;
     bool joined_ = false;
 };
 
