@@ -72,6 +72,16 @@ int main(int argc, char** argv) {
     hipEventElapsedTime(&ms, e0, e1);
     printf("trsm rows n=%d m=%d: %.1f us per call  (%.2f TFLOP/s)\n", n, m, ms * 1e3 / reps,
            double(n) * n * m / (ms * 1e-3 / reps) / 1e12);
+    // TRSM (wide: X = L^{-1} Y, the chain-round transform shape)
+    for (int it = 0; it < reps + 2; ++it) {
+        if (it == 2) hipEventRecord(e0, h->stream);
+        trsm(h, true, dW, dDi, n, dA, m, dX, m, m);
+    }
+    hipEventRecord(e1, h->stream);
+    hipStreamSynchronize(h->stream);
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("trsm cols n=%d m=%d: %.1f us per call  (%.2f TFLOP/s)\n", n, m, ms * 1e3 / reps,
+           double(n) * n * m / (ms * 1e-3 / reps) / 1e12);
     // check Cholesky residual on the host
     std::vector<double> L(G.size());
     hipMemcpy(L.data(), dW, L.size() * 8, hipMemcpyDeviceToHost);

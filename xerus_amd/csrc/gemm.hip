@@ -338,10 +338,10 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
         return;
     }
     // Tile choice (XRS_GEMM_CFG="variant,kmin,target" overrides for tuning experiments):
-    //   v1 128x128 (8 waves 2x4)              large problems (>= 240 tiles)
+    //   v1 128x128 (8 waves 2x4)              large problems
     //   v2  64x64  (8 waves 2x4)              mid-size
-    //   v3  64x32  (8 waves 2x2, K split 2)   TT "wide" shapes (M or N = r, other = n r): 2.5 tiles per CU
-    //   v4  32x32  (8 waves 2x2, K split 2)   + split-K for the r x r Gram shapes with K = n r
+    //   v3  64x32  (8 waves 2x2, K split 2)   split-K Gram shapes (r x r, K = n r)
+    //   v4  32x32  (8 waves 2x2, K split 2)   TT "wide"/"tall" shapes (M or N = r, other = n r)
     // split-K brings the grid to ~target workgroups while every split keeps >= kmin of K.
     static int cfg_var = 0, cfg_kmin = 256, cfg_target = 512;
     static bool cfg_read = false;
@@ -350,14 +350,31 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
         if (const char* e = std::getenv("XRS_GEMM_CFG")) std::sscanf(e, "%d,%d,%d", &cfg_var, &cfg_kmin, &cfg_target);
     }
     auto ntiles = [&](int bm, int bn) { return long((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+    const int bms[8] = {0, 128, 64, 64, 32, 64, 64, 64}, bns[8] = {0, 128, 64, 32, 32, 32, 64, 64};
     int var = cfg_var;
     if (var == 0) {
-        if (ntiles(128, 128) >= 240) var = 1;
+        // measured on the TT shapes (tools/gemm_tt_bench.py, profiles/r01/gemm_tt_sweep.txt):
+        //   256 x 5120 x 256 wide/tall: 32x32 24.8 us < 64x32 26.8 < 64x64 28.6 < 128x128 44.5 (alone;
+        //                               with 3 concurrent streams 64x32 wins, see below)
+        //   512 x 10240 x 512:          64x64 131 us < 64x32 148 < 128x128 154
+        //   Gram 256^2, K 5120:         64x32 x16 splits 29-31 us < 32x32 x8 34;
+        //   Gram 512^2, K 10240:        128x128 x32 splits 130 us < 32x32 x2 167
+        // so: no split while the grid has >= 512 tiles of some size (the largest such tile wins up to
+        // 64x64; 128x128 only from ~1000 tiles), else the largest tile whose split-K grid reaches
+        // `target` workgroups (fewer, larger tiles re-read less of the long-K operands).
+        if (ntiles(128, 128) >= 1000) var = 1;
         else if (ntiles(64, 64) >= 512) var = 2;
-        else if (ntiles(64, 32) >= 256) var = 3;
-        else var = 4;
+        else if (ntiles(64, 32) >= 256) var = 3;   // 32x32 is 2 us faster alone but 2x the workgroups:
+        else if (ntiles(32, 32) >= 512) var = 4;   // it starves the concurrent latency-bound TRSMs
+        else {
+            var = 4;
+            for (int v : {1, 2, 3}) {
+                const long t = ntiles(bms[v], bns[v]);
+                const long sp = std::min<long>((cfg_target + t - 1) / t, std::max<long>(1, K / cfg_kmin));
+                if (t * sp >= cfg_target) { var = v; break; }
+            }
+        }
     }
-    const int bms[8] = {0, 128, 64, 64, 32, 64, 64, 64}, bns[8] = {0, 128, 64, 32, 32, 32, 64, 64};
     const long tiles = ntiles(bms[var], bns[var]);
     int splits = 1;
     if (tiles < cfg_target) {

@@ -38,12 +38,17 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
 //       x D^T = g by substitution against D in LDS (one row per thread, 32 registers);
 //   (3) all waves apply the rank-32 trailing update from the LDS panel with 4x4 register tiles.
 __device__ __forceinline__ void potrf32_body(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
-                                             int* __restrict__ status, double* __restrict__ info) {
+                                             int* __restrict__ status, double* __restrict__ info,
+                                             const double* src = nullptr) {
     __shared__ double P[PMAX * (NB + 1)];
     __shared__ double Ds[NB][NB + 1];
     __shared__ double red[16];
     __shared__ int fail;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (src != nullptr && src != G) {   // out of place: this workgroup copies, then factors G in place
+        for (int e = tid; e < n * n; e += POT_THREADS) G[e] = src[e];
+        __syncthreads();
+    }
     double* dummy = Dinv + size_t(n + 31) * NB + (tid & 31);   // padding row of Dinv: sink for masked stores
     if (tid == 0) fail = 0;
     // trace(G) -> absolute shift (shift_rel * trace), no host round trip
@@ -382,7 +387,9 @@ __device__ __forceinline__ void trail_all(d4 (&acc)[PR_SLOTS], const int (&ti)[P
 }
 
 __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
-                                              int* __restrict__ status, double* __restrict__ info) {
+                                              int* __restrict__ status, double* __restrict__ info,
+                                              const double* __restrict__ src = nullptr) {
+    const double* __restrict__ S = src != nullptr ? src : G;   // read from S, L to G (if G is given)
     __shared__ double Dt[PTILE];
     __shared__ double Di[PTILE];
     __shared__ double P[PR_TMAX * PTILE];
@@ -397,7 +404,7 @@ __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, dou
     if (tid == 0) fail = 0;
     PSTAMP(0);
     double tr = 0.0;
-    for (int i = tid; i < n; i += PR_THREADS) tr += G[size_t(i) * n + i];
+    for (int i = tid; i < n; i += PR_THREADS) tr += S[size_t(i) * n + i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
     if (lane == 0) red[wave] = tr;
@@ -428,7 +435,7 @@ __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, dou
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = min(max(16 * i + lg + 4 * q, 0), n - 1), col = min(max(16 * k + lr, 0), n - 1);
-            acc[s][q] = G[size_t(row) * n + col];
+            acc[s][q] = S[size_t(row) * n + col];
         }
     }
 #pragma unroll
@@ -502,7 +509,7 @@ __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, dou
     asm volatile("" : "+v"(sg), "+v"(sr));
 #pragma unroll
     for (int s = 0; s < PR_SLOTS; ++s) {
-        if (ti[s] < 0) continue;
+        if (ti[s] < 0 || G == nullptr) continue;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int row = 16 * ti[s] + sg + 4 * q, col = 16 * tk[s] + sr;
@@ -525,12 +532,12 @@ __global__ void __launch_bounds__(PR_THREADS) k_potrf_rr(double* __restrict__ G,
 // Independent factorisations, one workgroup each (e.g. the Gram matrices of every TT edge).
 __global__ void __launch_bounds__(POT_THREADS) k_potrf32_batched(PotrfBatch b) {
     const int i = blockIdx.x;
-    potrf32_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr);
+    potrf32_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
 }
 
 __global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
     const int i = blockIdx.x;
-    potrf_rr_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr);
+    potrf_rr_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -973,6 +980,8 @@ void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count) {
         const bool rr = dinv_ld(b.n[i]) == 16;
         PotrfBatch& d = rr ? small : large;
         int& c = rr ? ns : nl;
+        XRS_REQUIRE(b.G[i] != nullptr || (rr && b.src[i] != nullptr), "potrf_batched: no input / output");
+        d.src[c] = b.src[i];
         d.G[c] = b.G[i];
         d.Dinv[c] = b.Dinv[i];
         d.shift[c] = b.shift[i];

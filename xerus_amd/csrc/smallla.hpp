@@ -14,6 +14,9 @@ void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int
 // own relative diagonal shift; status[i] as for potrf. Dinv[i] needs ceil(n_i/16)*256 doubles.
 constexpr int kPotrfBatchMax = 48;
 struct PotrfBatch {
+    // entry i factors src[i] (nullptr: G[i] in place) into G[i]; G[i] == nullptr (n <= 256 only): the
+    // factor is not stored (certificates: only the status is wanted)
+    const double* src[kPotrfBatchMax];
     double* G[kPotrfBatchMax];
     double* Dinv[kPotrfBatchMax];
     double shift[kPotrfBatchMax];

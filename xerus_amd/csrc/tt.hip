@@ -237,35 +237,37 @@ constexpr double kGramShift = 1e-11;
 // Gram chains from the current cores (k = 1..d-1, index k):
 //   left  G_k = X_{<k}^T X_{<k}:  G_1 = M_0^T M_0, G_{k+1} = M_k^T (G_k M_k)   (M_k: r_k x n_k r_{k+1})
 //   right H_k = X_{>=k} X_{>=k}^T: H_{d-1} = M M^T, H_k = M_k (I (x) H_{k+1}) M_k^T
-void left_grams(TT& t, std::vector<DevBuf>& G, double* T) {
-    const size_t d = t.d;
+void left_gram_step(TT& t, std::vector<DevBuf>& G, double* T, size_t k) {   // G_{k+1} from G_k (G_1 at k = 0)
     xrs_handle_t h = t.h;
-    gemm(h, G[1].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
-    t.reduce(G[1].d(), t.r[1] * t.r[1]);
-    for (size_t k = 1; k + 1 < d; ++k) {
-        const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-        gemm(h, T, a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
-        gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);
-        t.reduce(G[k + 1].d(), b * b);
+    if (k == 0) {
+        gemm(h, G[1].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
+        t.reduce(G[1].d(), t.r[1] * t.r[1]);
+        return;
     }
+    const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
+    gemm(h, T, a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
+    gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);
+    t.reduce(G[k + 1].d(), b * b);
 }
 
-void right_grams(TT& t, std::vector<DevBuf>& H, double* T) {
-    const size_t d = t.d;
+void right_gram_step(TT& t, std::vector<DevBuf>& H, double* T, size_t k) {   // H_k from H_{k+1} (H_{d-1} at k = d-1)
     xrs_handle_t h = t.h;
-    const size_t last = d - 1, cl = t.cols_right(last);
-    gemm(h, H[last].d(), t.r[last], t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
-    t.reduce(H[last].d(), t.r[last] * t.r[last]);
-    for (size_t k = last - 1; k >= 1; --k) {
-        const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-        gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
-        gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T, cols, true);         // M_k T^T
-        t.reduce(H[k].d(), a * a);
+    const size_t last = t.d - 1;
+    if (k == last) {
+        const size_t cl = t.cols_right(last);
+        gemm(h, H[last].d(), t.r[last], t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
+        t.reduce(H[last].d(), t.r[last] * t.r[last]);
+        return;
     }
+    const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
+    gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
+    gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T, cols, true);         // M_k T^T
+    t.reduce(H[k].d(), a * a);
 }
 
-// Both chains, concurrently: left on the side stream, right on the main stream (independent inputs;
-// every buffer they touch is allocated before the fork and outlives the join).
+// Both chains; unsharded they run concurrently (left on a side stream, right on the main stream) with
+// their launches interleaved step by step, so that neither stream waits for the host to finish
+// enqueueing the other chain. Every buffer they touch is allocated before the fork and outlives the join.
 void gram_chains(TT& t, std::vector<DevBuf>& G, std::vector<DevBuf>& H, bool left = true) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
@@ -280,20 +282,19 @@ void gram_chains(TT& t, std::vector<DevBuf>& G, std::vector<DevBuf>& H, bool lef
         H[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
     }
     DevBuf TL(h, tmax * 8), TR(h, tmax * 8);
-    if (!left) {
-        right_grams(t, H, TR.d());
-        return;
-    }
-    if (t.sharded()) {   // the all-reduce hook synchronises: keep the chains on one stream
-        left_grams(t, G, TL.d());
-        right_grams(t, H, TR.d());
+    if (!left || t.sharded()) {   // (the all-reduce hook synchronises: keep sharded chains on one stream)
+        if (left)
+            for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, TL.d(), k);
+        for (size_t k = d - 1; k >= 1; --k) right_gram_step(t, H, TR.d(), k);
         return;
     }
     StreamFork fork(h);
-    fork.side();
-    left_grams(t, G, TL.d());
-    fork.main();
-    right_grams(t, H, TR.d());
+    for (size_t s = 0; s + 1 < d; ++s) {
+        fork.side();
+        left_gram_step(t, G, TL.d(), s);
+        fork.main();
+        right_gram_step(t, H, TR.d(), d - 1 - s);
+    }
     fork.join();
 }
 
@@ -333,15 +334,23 @@ constexpr double kOrthTol = 1e-13;   // max |C_k C_k^T - I| accepted for the rig
 
 // One chain orthogonalisation pass over the current cores: the right Gram chain H_k (and, with
 // `certify`, the left chain G_k), ONE batched launch of all Cholesky factorisations -- H_k = L_k L_k^T
-// and, with `certify`, the down-shifted certificates of G_k and H_k -- then every core is transformed
-// independently: C_k = L_k^{-1} M_k (I (x) L_{k+1}), C_0 = M_0 (I (x) L_1). In exact arithmetic the
-// C_k (k >= 1) have orthonormal rows and represent the same tensor. Returns false (nothing allocated)
-// when a factorisation or certificate fails.
-bool chain_pass(TT& t, bool certify, std::vector<double*>& C) {
+// (out of place, into L_k) and, with `certify`, the down-shifted certificates of G_k and H_k (status
+// only) -- then every core is transformed independently: C_k = L_k^{-1} M_k (I (x) L_{k+1}),
+// C_0 = M_0 (I (x) L_1). In exact arithmetic the C_k (k >= 1) have orthonormal rows and represent the
+// same tensor. Nothing is synchronised: the factorisation statuses are copied to pinned host memory
+// behind the transforms and judged by chain_check (a failed factorisation only makes C garbage, which
+// is then discarded).
+struct ChainPass {
+    std::vector<double*> C;   // new cores (owned by the TT's pool until replaced / released)
+    int* status = nullptr;    // pinned host copy of the factorisation statuses
+    int count = 0;
+    bool certify = false;
+};
+
+void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
-    static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
-    std::vector<DevBuf> G, H, Hs(d);
+    std::vector<DevBuf> G, H, Lf(d), Cs;
     gram_chains(t, G, H, certify);
     const int per = certify ? 3 : 1;
     const int cnt = int(per * (d - 1));
@@ -349,20 +358,25 @@ bool chain_pass(TT& t, bool certify, std::vector<double*>& C) {
     for (size_t k = 1; k < d; ++k) dsz += dinv_elems(int(t.r[k]));
     DevBuf Dv(h, dsz * 8 + 8), Dscr(h, (certify ? 2 * dsz : 1) * 8 + 8), st(h, size_t(cnt) * 4 + 64);
     std::vector<double*> dinv(d, nullptr);
-    struct Job { double* G; double* Dinv; double shift; int n; };
+    struct Job { const double* src; double* G; double* Dinv; double shift; int n; };
     std::vector<Job> jobs;
     size_t off = 0;
     for (size_t k = 1; k < d; ++k) {
         const size_t a = t.r[k], de = dinv_elems(int(a));
         dinv[k] = Dv.d() + off;
-        if (certify) {
-            Hs[k] = DevBuf(h, a * a * 8);
-            XRS_HIP(hipMemcpyAsync(Hs[k].d(), H[k].d(), a * a * 8, hipMemcpyDeviceToDevice, h->stream));
-        }
-        jobs.push_back({H[k].d(), dinv[k], 0.0, int(a)});
-        if (certify) {
-            jobs.push_back({G[k].d(), Dscr.d() + 2 * off, -kGramShift, int(a)});
-            jobs.push_back({Hs[k].d(), Dscr.d() + 2 * off + de, -kGramShift, int(a)});
+        Lf[k] = DevBuf(h, a * a * 8);
+        jobs.push_back({H[k].d(), Lf[k].d(), dinv[k], 0.0, int(a)});
+        if (certify) {   // status-only certificates (the 32-block kernel for n > 256 needs a work copy)
+            double* w1 = nullptr;
+            double* w2 = nullptr;
+            if (a > 256) {
+                Cs.emplace_back(h, a * a * 8);
+                w1 = Cs.back().d();
+                Cs.emplace_back(h, a * a * 8);
+                w2 = Cs.back().d();
+            }
+            jobs.push_back({G[k].d(), w1, Dscr.d() + 2 * off, -kGramShift, int(a)});
+            jobs.push_back({H[k].d(), w2, Dscr.d() + 2 * off + de, -kGramShift, int(a)});
         }
         off += de;
     }
@@ -370,6 +384,7 @@ bool chain_pass(TT& t, bool certify, std::vector<double*>& C) {
         PotrfBatch pb{};
         const int c = std::min(kPotrfBatchMax, cnt - b0);
         for (int i = 0; i < c; ++i) {
+            pb.src[i] = jobs[b0 + i].src;
             pb.G[i] = jobs[b0 + i].G;
             pb.Dinv[i] = jobs[b0 + i].Dinv;
             pb.shift[i] = jobs[b0 + i].shift;
@@ -378,44 +393,50 @@ bool chain_pass(TT& t, bool certify, std::vector<double*>& C) {
         pb.status = st.as<int>() + b0;
         potrf_batched(h, pb, c);
     }
-    int* hs = static_cast<int*>(h->host_scratch);
-    XRS_HIP(hipMemcpyAsync(hs, st.d(), size_t(cnt) * 4, hipMemcpyDeviceToHost, h->stream));
-    XRS_HIP(hipStreamSynchronize(h->stream));
-    for (int i = 0; i < cnt; ++i)
-        if (hs[i] != 0) {
+    XRS_HIP(hipMemcpyAsync(host_status, st.d(), size_t(cnt) * 4, hipMemcpyDeviceToHost, h->stream));
+    out.status = host_status;
+    out.count = cnt;
+    out.certify = certify;
+    // the d transforms are independent: spread them over the main and side streams (buffers they share
+    // with the rest of the round are allocated before the fork and released after the join)
+    out.C.assign(d, nullptr);
+    std::vector<DevBuf> W(d);
+    for (size_t k = 0; k < d; ++k) {
+        out.C[k] = t.alloc(t.size(k));
+        if (k > 0 && k + 1 < d) W[k] = DevBuf(h, t.size(k) * 8);
+    }
+    StreamFork fork(h, xrs_handle_s::kSides);
+    for (size_t k = 0; k < d; ++k) {
+        fork.lane(int(k % size_t(fork.lanes())));
+        const size_t a = t.r[k], b = t.r[k + 1], rows = t.rows_left(k), cols = t.cols_right(k);
+        const double* src = t.core[k];
+        if (k + 1 < d) {   // M_k (I (x) L_{k+1}): (r_k n_k) x r_{k+1} times r_{k+1} x r_{k+1}
+            gemm(h, k == 0 ? out.C[k] : W[k].d(), rows, b, 1.0, t.core[k], b, false, b, Lf[k + 1].d(), b, false);
+            src = W[k].d();
+        }
+        if (k > 0) trsm(h, true, Lf[k].d(), dinv[k], int(a), src, cols, out.C[k], cols, int(cols));
+        else if (k + 1 == d) XRS_HIP(hipMemcpyAsync(out.C[k], src, t.size(k) * 8, hipMemcpyDeviceToDevice, h->stream));
+    }
+    fork.join();
+}
+
+// True when every factorisation of the pass succeeded (valid after the stream has been synchronised).
+bool chain_status_ok(const ChainPass& p) {
+    static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
+    const int per = p.certify ? 3 : 1;
+    for (int i = 0; i < p.count; ++i)
+        if (p.status[i] != 0) {
             if (dbg)
                 std::fprintf(stderr, "chain_pass: Cholesky %d of edge %d (%s) failed at column %d\n", i, i / per + 1,
                              i % per == 0 ? "right factor" : (i % per == 1 ? "left certificate" : "right certificate"),
-                             hs[i]);
+                             p.status[i]);
             return false;
         }
-    // the d transforms are independent: spread them over the main and side streams (buffers they share
-    // with the rest of the round are allocated before the fork and released after the join)
-    C.assign(d, nullptr);
-    std::vector<DevBuf> W(d);
-    for (size_t k = 0; k < d; ++k) {
-        C[k] = t.alloc(t.size(k));
-        if (k > 0 && k + 1 < d) W[k] = DevBuf(h, t.size(k) * 8);
-    }
-    {
-        StreamFork fork(h, xrs_handle_s::kSides);
-        for (size_t k = 0; k < d; ++k) {
-            fork.lane(int(k % size_t(fork.lanes())));
-            const size_t a = t.r[k], b = t.r[k + 1], rows = t.rows_left(k), cols = t.cols_right(k);
-            const double* src = t.core[k];
-            if (k + 1 < d) {   // M_k (I (x) L_{k+1}): (r_k n_k) x r_{k+1} times r_{k+1} x r_{k+1}
-                gemm(h, k == 0 ? C[k] : W[k].d(), rows, b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);
-                src = W[k].d();
-            }
-            if (k > 0) trsm(h, true, H[k].d(), dinv[k], int(a), src, cols, C[k], cols, int(cols));
-            else if (k + 1 == d) XRS_HIP(hipMemcpyAsync(C[k], src, t.size(k) * 8, hipMemcpyDeviceToDevice, h->stream));
-        }
-        fork.join();
-    }
     return true;
 }
 
-// max_k max |C_k C_k^T - I| over cores 1..d-1 (mode sums completed across ranks when sharded)
+// max_k max |C_k C_k^T - I| over cores 1..d-1 (mode sums completed across ranks when sharded).
+// Synchronises the stream (so the pass statuses are readable afterwards).
 double chain_check(TT& t, const std::vector<double*>& C) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
@@ -461,6 +482,7 @@ double chain_check(TT& t, const std::vector<double*>& C) {
 // kappa^2 u, so an ill-conditioned input (e.g. a square unfolding) can miss the 1e-13 bar: pass 2
 // repeats the right chain on the pass-1 cores (now near-orthonormal, so the chain is well conditioned)
 // -- CholeskyQR2 applied to the whole train. Only if that also fails does the sequential sweep run.
+// One host synchronisation per pass (the check).
 bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
     static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
@@ -469,24 +491,31 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
         if (t.r[k] > max_ranks[k - 1] || t.r[k] > size_t(kSmallMax)) return false;
     const double cX = 0.5 * std::sqrt(kGramShift);
     if (!(eps < 0.25 * cX * cX)) return false;
-    std::vector<double*> C;
-    if (!chain_pass(t, true, C)) return false;
-    double dev = chain_check(t, C);
+    // factorisation statuses (<= 3*64 ints) in a region of the pinned scratch no other routine uses
+    int* hs = static_cast<int*>(t.h->host_scratch) + 12288;
+    ChainPass p1;
+    chain_pass(t, true, p1, hs);
+    double dev = chain_check(t, p1.C);
+    if (!chain_status_ok(p1)) {
+        for (size_t k = 0; k < d; ++k) t.release(p1.C[k]);
+        return false;
+    }
+    std::vector<double*> C = p1.C;
     if (!(dev <= kOrthTol)) {
         if (dbg) std::fprintf(stderr, "round_chain: pass 1 orthogonality %.3e, second pass\n", dev);
         TT t2 = t;
         t2.core = C.data();
-        std::vector<double*> C2;
-        if (chain_pass(t2, false, C2)) {
-            const double dev2 = chain_check(t2, C2);
-            if (dbg) std::fprintf(stderr, "round_chain: pass 2 orthogonality %.3e\n", dev2);
-            if (dev2 <= kOrthTol) {
-                for (size_t k = 0; k < d; ++k) t.release(C[k]);
-                C = C2;
-                dev = dev2;
-            } else {
-                for (size_t k = 0; k < d; ++k) t.release(C2[k]);
-            }
+        ChainPass p2;
+        chain_pass(t2, false, p2, hs);
+        const double dev2 = chain_check(t2, p2.C);
+        const bool ok2 = chain_status_ok(p2);
+        if (dbg) std::fprintf(stderr, "round_chain: pass 2 orthogonality %.3e (factors %s)\n", dev2, ok2 ? "ok" : "failed");
+        if (ok2 && dev2 <= kOrthTol) {
+            for (size_t k = 0; k < d; ++k) t.release(C[k]);
+            C = p2.C;
+            dev = dev2;
+        } else {
+            for (size_t k = 0; k < d; ++k) t.release(p2.C[k]);
         }
     }
     const bool ok = dev <= kOrthTol;
