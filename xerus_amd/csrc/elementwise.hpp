@@ -22,6 +22,10 @@ void strided_eval(xrs_handle_t h, double* out, const double* in, size_t nd, cons
 // gemm.hip
 void gemm(xrs_handle_t h, double* C, size_t M, size_t N, double alpha, const double* A, size_t lda, bool ta, size_t K,
           const double* B, size_t ldb, bool tb);
+// Batch of same-shape GEMMs C[i] = alpha op(A[i]) op(B[i]) in one launch per kGemmBatchMax entries
+constexpr int kGemmBatchMax = 32;
+void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t M, size_t N, double alpha, const double* const* A,
+                  size_t lda, bool ta, size_t K, const double* const* B, size_t ldb, bool tb);
 
 // permute.hip
 void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const size_t* dims, const size_t* shuffle);

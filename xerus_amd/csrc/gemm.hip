@@ -17,17 +17,41 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "elementwise.hpp"
 #include "runtime.hpp"
 
 namespace xrs {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB>
+// Operand tables: one GEMM, or a batch of same-shape GEMMs (blockIdx.y = batch entry) in one launch.
+struct GemmOne {
+    const double* A;
+    const double* B;
+    double* C;
+    __device__ const double* a(int) const { return A; }
+    __device__ const double* b(int) const { return B; }
+    __device__ double* c(int) const { return C; }
+};
+struct GemmMany {
+    const double* A[kGemmBatchMax];
+    const double* B[kGemmBatchMax];
+    double* C[kGemmBatchMax];
+    __device__ const double* a(int i) const { return A[i]; }
+    __device__ const double* b(int i) const { return B[i]; }
+    __device__ double* c(int i) const { return C[i]; }
+};
+
+template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB, class PTR>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64, (WGM * WGN * WGK * 64 * 2 <= 1024) ? 2 : 1)
-k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ B, size_t ldb,
-           double* __restrict__ C, int M, int N, int K, int kps, double alpha, double* __restrict__ slab,
-           int tiles_m, int xcd_group, int* __restrict__ tickets) {
+k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
+           double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets) {
+    const int bz = blockIdx.y;   // batch entry
+    const double* __restrict__ A = ptrs.a(bz);
+    const double* __restrict__ B = ptrs.b(bz);
+    double* __restrict__ C = ptrs.c(bz);
+    const int zslice = bz * int(gridDim.z) + int(blockIdx.z);   // this slice's slab index
+    const int tslot = bz * int(gridDim.x) + int(blockIdx.x);    // this tile's ticket
     constexpr int NT = WGM * WGN * WGK * 64;   // WGK wave groups split every K-step's MFMA k-substeps
     // LDS rows of BM / BN doubles, XOR-swizzled per k row: element (k, m) at k*SA + (m ^ swz(k)) with
     // swz(k) = 16*(k&1) + (k>>1). Fragment reads (lanes: 16 m x rows k, k+1) hit 32 distinct bank pairs
@@ -235,7 +259,7 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
     // ---- epilogue
     const bool to_slab = slab != nullptr;
     const size_t MN = size_t(M) * size_t(N);
-    double* out = to_slab ? slab + size_t(blockIdx.z) * MN : C;
+    double* out = to_slab ? slab + size_t(zslice) * MN : C;
     const double scale = to_slab ? 1.0 : alpha;
     const int lc = lane & 15, lg = lane >> 4;
     if (kg == 0) {
@@ -266,9 +290,9 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
     __syncthreads();
     double* flag = &As[0][0];   // the one LDS array (no second __shared__ object, see the guide's trap 4a)
     if (tid == 0) {
-        const int t = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int t = __hip_atomic_fetch_add(&tickets[tslot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = (t == int(gridDim.z) - 1);
-        if (last) __hip_atomic_store(&tickets[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) __hip_atomic_store(&tickets[tslot], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = last ? 1.0 : 0.0;
     }
     __syncthreads();
@@ -286,7 +310,7 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
                     double sum = 0.0;
                     for (int z = 0; z < int(gridDim.z); ++z)
                         sum += (z == int(blockIdx.z)) ? acc[i][j][r]
-                                                      : __hip_atomic_load(&slab[size_t(z) * MN + o], __ATOMIC_RELAXED,
+                                                      : __hip_atomic_load(&slab[(size_t(bz) * gridDim.z + z) * MN + o], __ATOMIC_RELAXED,
                                                                           __HIP_MEMORY_SCOPE_AGENT);
                     C[o] = alpha * sum;
                 }
@@ -294,8 +318,11 @@ k_gemm_f64(const double* __restrict__ A, size_t lda, const double* __restrict__ 
         }
 }
 
-__global__ void __launch_bounds__(256) k_splitk_reduce(double* __restrict__ C, const double* __restrict__ slab, size_t MN,
+template <class PTR>
+__global__ void __launch_bounds__(256) k_splitk_reduce(const PTR ptrs, const double* __restrict__ slab, size_t MN,
                                                        int splits, double alpha) {
+    double* __restrict__ C = ptrs.c(blockIdx.y);
+    slab += size_t(blockIdx.y) * splits * MN;
     const size_t stride = size_t(gridDim.x) * blockDim.x;
     for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < MN; i += stride) {
         double s = 0.0;
@@ -304,22 +331,22 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(double* __restrict__ C, c
     }
 }
 
-template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD>
-static void launch_tiles(xrs_handle_t h, const double* A, size_t lda, bool ta, const double* B, size_t ldb, bool tb,
-                         double* C, int M, int N, int K, int splits, int kps, double alpha, double* slab, int* tickets) {
+template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, class PTR>
+static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bool ta, size_t ldb, bool tb,
+                         int M, int N, int K, int splits, int kps, double alpha, double* slab, int* tickets) {
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
-    dim3 grid(unsigned(tiles_m * tiles_n), 1, unsigned(splits));
+    dim3 grid(unsigned(tiles_m * tiles_n), unsigned(count), unsigned(splits));
     // group by the larger operand's panels (B: K x N, A: M x K) when the tile grid allows a bijection
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
     static const bool noxcd = std::getenv("XRS_GEMM_NOXCD") != nullptr;
     if (noxcd) xg = 0;
-    KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(M) * double(N) * double(K),
-                      8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
+    KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * double(K),
+                      count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GEMM_LAUNCH(TA_, TB_)                                                                             \
-    hipLaunchKernelGGL((k_gemm_f64<BM, BN, GBK, WGM, WGN, WGK, PD, TA_, TB_>), grid, dim3(WGM * WGN * WGK * 64), 0, h->stream, A, lda, B, ldb, C, M, N, K, \
-                       kps, alpha, slab, tiles_m, xg, tickets)
+    hipLaunchKernelGGL((k_gemm_f64<BM, BN, GBK, WGM, WGN, WGK, PD, TA_, TB_, PTR>), grid, dim3(WGM * WGN * WGK * 64), 0, \
+                       h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets)
     if (!ta && !tb) XRS_GEMM_LAUNCH(false, false);
     else if (!ta && tb) XRS_GEMM_LAUNCH(false, true);
     else if (ta && !tb) XRS_GEMM_LAUNCH(true, false);
@@ -328,15 +355,10 @@ static void launch_tiles(xrs_handle_t h, const double* A, size_t lda, bool ta, c
     check_launch("k_gemm_f64");
 }
 
-void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const double* A, size_t lda, bool ta, size_t Ks,
-          const double* B, size_t ldb, bool tb) {
-    if (Ms == 0 || Ns == 0) return;
-    XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
+template <class PTR>
+static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t Ns, double alpha, size_t lda, bool ta,
+                      size_t Ks, size_t ldb, bool tb) {
     const int M = int(Ms), N = int(Ns), K = int(Ks);
-    if (K == 0) {
-        XRS_HIP(hipMemsetAsync(C, 0, size_t(M) * N * 8, h->stream));
-        return;
-    }
     // Tile choice (XRS_GEMM_CFG="variant,kmin,target" overrides for tuning experiments):
     //   v1 128x128 (8 waves 2x4)              large problems
     //   v2  64x64  (8 waves 2x4)              mid-size
@@ -349,7 +371,8 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
         cfg_read = true;
         if (const char* e = std::getenv("XRS_GEMM_CFG")) std::sscanf(e, "%d,%d,%d", &cfg_var, &cfg_kmin, &cfg_target);
     }
-    auto ntiles = [&](int bm, int bn) { return long((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
+    // (batched: the tile counts are over the whole batch)
+    auto ntiles = [&](int bm, int bn) { return long(count) * ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     const int bms[8] = {0, 128, 64, 64, 32, 64, 64, 64}, bns[8] = {0, 128, 64, 32, 32, 32, 64, 64};
     int var = cfg_var;
     if (var == 0) {
@@ -386,8 +409,9 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
     int kps = (K + splits - 1) / splits;
     kps = (kps + bk - 1) / bk * bk;
     splits = (K + kps - 1) / kps;
+    if (std::is_same<PTR, GemmMany>::value && var >= 5) var = (var == 5) ? 3 : 2;   // tuning-only tiles: single GEMMs
     DevBuf slab;
-    if (splits > 1) slab = DevBuf(h, size_t(splits) * M * N * sizeof(double));
+    if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
     // one-launch split-K when the tile grid fits the stream's ticket array (XRS_GEMM_SPLITK2=1: old
     // two-kernel form, for A/B timing)
     static const bool two_kernel = std::getenv("XRS_GEMM_SPLITK2") != nullptr;
@@ -396,21 +420,55 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
     const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= 65536;
     int* tickets = (splits > 1 && !two_kernel && small_slab && ntiles(bms[var], bns[var]) <= xrs_handle_s::kTicketCap)
                        ? h->tickets : nullptr;
+#define XRS_TILES(...) launch_tiles<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets)
     switch (var) {
-        case 1: launch_tiles<128, 128, 16, 2, 4, 1, 2>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
-        case 2: launch_tiles<64, 64, 16, 2, 4, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
-        case 3: launch_tiles<64, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
-        case 5: launch_tiles<64, 32, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
-        case 6: launch_tiles<64, 64, 32, 2, 2, 1, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
-        case 7: launch_tiles<64, 64, 32, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
-        default: launch_tiles<32, 32, 16, 2, 2, 2, 4>(h, A, lda, ta, B, ldb, tb, C, M, N, K, splits, kps, alpha, slab.d(), tickets); break;
+        case 1: XRS_TILES(128, 128, 16, 2, 4, 1, 2); break;
+        case 2: XRS_TILES(64, 64, 16, 2, 4, 1, 4); break;
+        case 3: XRS_TILES(64, 32, 16, 2, 2, 2, 4); break;
+        case 5: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 32, 32, 2, 2, 2, 4); break;
+        case 6: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 64, 32, 2, 2, 1, 4); break;
+        case 7: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 64, 32, 2, 2, 2, 4); break;
+        default: XRS_TILES(32, 32, 16, 2, 2, 2, 4); break;
     }
+#undef XRS_TILES
     if (splits > 1 && tickets == nullptr) {
         const size_t MN = size_t(M) * N;
         const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
-        KernelTimer timer(h, XRS_KFAM_ELEMWISE, double(MN) * splits, 8.0 * double(MN) * (splits + 1));
-        hipLaunchKernelGGL(k_splitk_reduce, dim3(blocks), dim3(256), 0, h->stream, C, slab.d(), MN, splits, alpha);
+        KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
+        hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab.d(), MN,
+                           splits, alpha);
         check_launch("k_splitk_reduce");
+    }
+}
+
+void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const double* A, size_t lda, bool ta, size_t Ks,
+          const double* B, size_t ldb, bool tb) {
+    if (Ms == 0 || Ns == 0) return;
+    XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
+    if (Ks == 0) {
+        XRS_HIP(hipMemsetAsync(C, 0, Ms * Ns * 8, h->stream));
+        return;
+    }
+    gemm_impl(h, GemmOne{A, B, C}, 1, Ms, Ns, alpha, lda, ta, Ks, ldb, tb);
+}
+
+void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t Ns, double alpha, const double* const* A,
+                  size_t lda, bool ta, size_t Ks, const double* const* B, size_t ldb, bool tb) {
+    if (Ms == 0 || Ns == 0 || count <= 0) return;
+    XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
+    if (Ks == 0) {
+        for (int i = 0; i < count; ++i) XRS_HIP(hipMemsetAsync(C[i], 0, Ms * Ns * 8, h->stream));
+        return;
+    }
+    for (int b0 = 0; b0 < count; b0 += kGemmBatchMax) {
+        const int c = std::min(kGemmBatchMax, count - b0);
+        GemmMany P{};
+        for (int i = 0; i < c; ++i) {
+            P.A[i] = A[b0 + i];
+            P.B[i] = B[b0 + i];
+            P.C[i] = C[b0 + i];
+        }
+        gemm_impl(h, P, c, Ms, Ns, alpha, lda, ta, Ks, ldb, tb);
     }
 }
 

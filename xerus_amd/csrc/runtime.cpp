@@ -182,6 +182,7 @@ int xrs_create(xrs_handle_t* handle, int device) {
             XRS_HIP(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
         }
         XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+        XRS_HIP(hipEventCreateWithFlags(&h->ev_aux, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
         const size_t tbytes = size_t(1 + xrs_handle_s::kSides) * xrs_handle_s::kTicketCap * sizeof(int);
@@ -213,6 +214,7 @@ int xrs_destroy(xrs_handle_t h) {
             if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
         }
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+        if (h->ev_aux) (void)hipEventDestroy(h->ev_aux);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
         (void)hipFree(h->ticket_base);

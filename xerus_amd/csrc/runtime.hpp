@@ -93,6 +93,7 @@ struct xrs_handle_s {
     hipStream_t side_stream[kSides] = {};
     xrs::Pool* side_pool[kSides] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kSides] = {};
+    hipEvent_t ev_aux = nullptr;   // one extra cross-stream dependency inside a fork (see tt.hip chain_pass)
     // split-K arrival tickets (zero between launches; the last arriving slice resets its word), one
     // array per stream so concurrent launches never share a word; `tickets` follows `stream`
     static constexpr int kTicketCap = 4096;

@@ -549,24 +549,27 @@ __global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
 // ahead (register prefetch). Dinv: 16x16 diagonal-block inverses; dld = 16 (k_potrf_rr layout,
 // block J at Dinv + 256 J) or 32 (k_potrf layout: the 16x16 diagonal sub-blocks of the 32x32 block
 // inverses are the 16-block inverses).
+// RHS vectors v0 .. v0+15 of X = L^{-1} Y; ident: Y = I (n x n, COLS), i.e. 16 columns of L^{-1}.
 template <bool COLS, int TMAX>
-__global__ void __launch_bounds__(256) k_trsm16(const double* __restrict__ L, const double* __restrict__ Dinv, int dld,
-                                                int n, const double* __restrict__ Y, size_t ldy, double* __restrict__ X,
-                                                size_t ldx, int nvec) {
+__device__ __forceinline__ void trsm16_body(const double* __restrict__ L, const double* __restrict__ Dinv, int dld,
+                                            int n, const double* __restrict__ Y, size_t ldy, double* __restrict__ X,
+                                            size_t ldx, int nvec, int v0, bool ident) {
     constexpr int JS = TMAX / 4;
     __shared__ double Xs[TMAX * 16 * PT];
     __shared__ double red[2][4][256];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 15, lg = lane >> 4;
-    const int v0 = blockIdx.x * 16;
     const int T = (n + 15) >> 4;
     const int np = T * 16;
     for (int e = tid; e < np * 16; e += 256) {
         int i, v;
         if (COLS) { i = e >> 4; v = e & 15; } else { v = e / np; i = e - v * np; }
         double y = 0.0;
-        if (i < n && v0 + v < nvec) y = COLS ? Y[size_t(i) * ldy + v0 + v] : Y[size_t(v0 + v) * ldy + i];
+        if (i < n && v0 + v < nvec) {
+            if (ident) y = (i == v0 + v) ? 1.0 : 0.0;
+            else y = COLS ? Y[size_t(i) * ldy + v0 + v] : Y[size_t(v0 + v) * ldy + i];
+        }
         Xs[i * PT + v] = y;
     }
     auto dinv_at = [&](int I, int c) -> double {
@@ -645,10 +648,26 @@ __global__ void __launch_bounds__(256) k_trsm16(const double* __restrict__ L, co
         int i, v;
         if (COLS) { i = e >> 4; v = e & 15; } else { v = e / np; i = e - v * np; }
         if (i < n && v0 + v < nvec) {
-            if (COLS) X[size_t(i) * ldx + v0 + v] = Xs[i * PT + v];
-            else X[size_t(v0 + v) * ldx + i] = Xs[i * PT + v];
+            const double x = (ident && i < v0 + v) ? 0.0 : Xs[i * PT + v];   // L^{-1}: exact zero upper triangle
+            if (COLS) X[size_t(i) * ldx + v0 + v] = x;
+            else X[size_t(v0 + v) * ldx + i] = x;
         }
     }
+}
+
+template <bool COLS, int TMAX>
+__global__ void __launch_bounds__(256) k_trsm16(const double* __restrict__ L, const double* __restrict__ Dinv, int dld,
+                                                int n, const double* __restrict__ Y, size_t ldy, double* __restrict__ X,
+                                                size_t ldx, int nvec) {
+    trsm16_body<COLS, TMAX>(L, Dinv, dld, n, Y, ldy, X, ldx, nvec, int(blockIdx.x) * 16, false);
+}
+
+// Batched triangular inverses X_i = L_i^{-1} (n_i x n_i, lower; blockIdx.y = matrix, blockIdx.x = 16 columns)
+template <int TMAX>
+__global__ void __launch_bounds__(256) k_trinv_batched(const TrinvBatch b, int dld) {
+    const int i = blockIdx.y, n = b.n[i];
+    if (int(blockIdx.x) * 16 >= n) return;
+    trsm16_body<true, TMAX>(b.L[i], b.Dinv[i], dld, n, nullptr, 0, b.X[i], size_t(n), n, int(blockIdx.x) * 16, true);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1032,6 +1051,33 @@ void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n,
     }
 #undef XRS_TRSM
     check_launch("k_trsm16");
+}
+
+void trinv_batched(xrs_handle_t h, const TrinvBatch& b, int count) {
+    XRS_REQUIRE(count >= 0 && count <= kTrinvBatchMax, "trinv_batched: batch too large");
+    // one launch per Dinv layout (n <= 256: 16-blocks, else 32-blocks), as in potrf_batched
+    for (int big = 0; big < 2; ++big) {
+        TrinvBatch g{};
+        int c = 0, nmax = 0;
+        double fl = 0.0;
+        for (int i = 0; i < count; ++i) {
+            XRS_REQUIRE(b.n[i] >= 1 && b.n[i] <= PMAX, "trinv_batched: n out of range");
+            if ((dinv_ld(b.n[i]) == 32) != bool(big)) continue;
+            g.L[c] = b.L[i];
+            g.Dinv[c] = b.Dinv[i];
+            g.X[c] = b.X[i];
+            g.n[c] = b.n[i];
+            nmax = std::max(nmax, b.n[i]);
+            fl += double(b.n[i]) * b.n[i] * b.n[i];
+            ++c;
+        }
+        if (c == 0) continue;
+        KernelTimer timer(h, XRS_KFAM_QR, fl, 0.0);
+        const dim3 grid(unsigned((nmax + 15) / 16), unsigned(c));
+        if (big) hipLaunchKernelGGL((k_trinv_batched<32>), grid, dim3(256), 0, h->stream, g, 32);
+        else hipLaunchKernelGGL((k_trinv_batched<16>), grid, dim3(256), 0, h->stream, g, 16);
+        check_launch("k_trinv_batched");
+    }
 }
 
 size_t qrcp(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C, bool pivot, bool abs_r00,

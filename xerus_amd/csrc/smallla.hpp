@@ -26,6 +26,16 @@ struct PotrfBatch {
 void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count);
 // doubles needed for the Dinv output of potrf / potrf_batched for an n x n matrix
 size_t dinv_elems(int n);
+// Batch of explicit inverses X_i = L_i^{-1} of lower-triangular factors from potrf / potrf_batched
+// (Dinv_i their diagonal-block inverses); X_i is n_i x n_i, upper triangle zero. One launch per Dinv layout.
+constexpr int kTrinvBatchMax = 64;
+struct TrinvBatch {
+    const double* L[kTrinvBatchMax];
+    const double* Dinv[kTrinvBatchMax];
+    double* X[kTrinvBatchMax];
+    int n[kTrinvBatchMax];
+};
+void trinv_batched(xrs_handle_t h, const TrinvBatch& b, int count);
 // X = L^{-1} Y. cols=false: the RHS vectors are the nvec rows of Y (ld ldy); cols=true: the nvec columns.
 void trsm(xrs_handle_t h, bool cols, const double* L, const double* Dinv, int n, const double* Y, size_t ldy, double* X,
           size_t ldx, int nvec);

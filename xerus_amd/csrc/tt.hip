@@ -17,9 +17,11 @@
 // max_rank >= r, no singular value can be cut, so the SVD is skipped and B = L Q is used directly:
 // same represented tensor, same ranks, different (equally valid) orthogonal gauge.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
+#include <string>
 #include <vector>
 
 #include "smallla.hpp"
@@ -298,6 +300,27 @@ void gram_chains(TT& t, std::vector<DevBuf>& G, std::vector<DevBuf>& H, bool lef
     fork.join();
 }
 
+// Host-side phase timestamps of round() (XRS_ROUND_TIMING=1: one stderr line per round; diagnostics only)
+struct HostMarks {
+    bool on = std::getenv("XRS_ROUND_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    std::string line;
+    void mark(const char* what) {
+        if (!on) return;
+        const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        char buf[64];
+        std::snprintf(buf, sizeof(buf), " %s %.0f", what, us);
+        line += buf;
+    }
+    ~HostMarks();
+};
+HostMarks* g_marks = nullptr;
+HostMarks::~HostMarks() {
+    if (g_marks == this) g_marks = nullptr;
+    if (on) std::fprintf(stderr, "[round host us]%s\n", line.c_str());
+}
+#define XRS_MARK(what) do { if (g_marks) g_marks->mark(what); } while (0)
+
 struct DevIdArgs {
     const double* G[64];
     int n[64];
@@ -340,6 +363,37 @@ constexpr double kOrthTol = 1e-13;   // max |C_k C_k^T - I| accepted for the rig
 // same tensor. Nothing is synchronised: the factorisation statuses are copied to pinned host memory
 // behind the transforms and judged by chain_check (a failed factorisation only makes C garbage, which
 // is then discarded).
+// Independent GEMMs; the ones of identical shape go out as one batched launch.
+struct GemmJob {
+    size_t M, N, K, lda, ldb;
+    bool ta, tb;
+    const double* A;
+    const double* B;
+    double* C;
+};
+
+void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
+    std::vector<bool> done(jobs.size(), false);
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        if (done[i]) continue;
+        const GemmJob& g = jobs[i];
+        std::vector<const double*> A, B;
+        std::vector<double*> C;
+        for (size_t j = i; j < jobs.size(); ++j) {
+            const GemmJob& o = jobs[j];
+            if (done[j] || o.M != g.M || o.N != g.N || o.K != g.K || o.lda != g.lda || o.ldb != g.ldb || o.ta != g.ta ||
+                o.tb != g.tb)
+                continue;
+            done[j] = true;
+            A.push_back(o.A);
+            B.push_back(o.B);
+            C.push_back(o.C);
+        }
+        if (C.size() == 1) gemm(h, C[0], g.M, g.N, 1.0, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
+        else gemm_batched(h, int(C.size()), C.data(), g.M, g.N, 1.0, A.data(), g.lda, g.ta, g.K, B.data(), g.ldb, g.tb);
+    }
+}
+
 struct ChainPass {
     std::vector<double*> C;   // new cores (owned by the TT's pool until replaced / released)
     int* status = nullptr;    // pinned host copy of the factorisation statuses
@@ -351,7 +405,9 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
     std::vector<DevBuf> G, H, Lf(d), Cs;
+    XRS_MARK("pass");
     gram_chains(t, G, H, certify);
+    XRS_MARK("chains");
     const int per = certify ? 3 : 1;
     const int cnt = int(per * (d - 1));
     size_t dsz = 0;
@@ -394,30 +450,53 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
         potrf_batched(h, pb, c);
     }
     XRS_HIP(hipMemcpyAsync(host_status, st.d(), size_t(cnt) * 4, hipMemcpyDeviceToHost, h->stream));
+    XRS_MARK("potrf");
     out.status = host_status;
     out.count = cnt;
     out.certify = certify;
-    // the d transforms are independent: spread them over the main and side streams (buffers they share
-    // with the rest of the round are allocated before the fork and released after the join)
+    // The d transforms are independent: same-shape GEMMs go out as one batched launch each, all on the
+    // main stream (cross-stream event hops cost ~20 us each here; a batch fills the chip as well as
+    // concurrent streams do). The left factor is applied as a GEMM with the explicit inverse
+    // Z_k = L_k^{-1} (one batched launch); the check below certifies the result either way.
     out.C.assign(d, nullptr);
-    std::vector<DevBuf> W(d);
+    std::vector<DevBuf> W(d), Z(d);
+    TrinvBatch tb{};
+    int ninv = 0;
     for (size_t k = 0; k < d; ++k) {
         out.C[k] = t.alloc(t.size(k));
         if (k > 0 && k + 1 < d) W[k] = DevBuf(h, t.size(k) * 8);
-    }
-    StreamFork fork(h, xrs_handle_s::kSides);
-    for (size_t k = 0; k < d; ++k) {
-        fork.lane(int(k % size_t(fork.lanes())));
-        const size_t a = t.r[k], b = t.r[k + 1], rows = t.rows_left(k), cols = t.cols_right(k);
-        const double* src = t.core[k];
-        if (k + 1 < d) {   // M_k (I (x) L_{k+1}): (r_k n_k) x r_{k+1} times r_{k+1} x r_{k+1}
-            gemm(h, k == 0 ? out.C[k] : W[k].d(), rows, b, 1.0, t.core[k], b, false, b, Lf[k + 1].d(), b, false);
-            src = W[k].d();
+        if (k > 0) {
+            Z[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
+            tb.L[ninv] = Lf[k].d();
+            tb.Dinv[ninv] = dinv[k];
+            tb.X[ninv] = Z[k].d();
+            tb.n[ninv] = int(t.r[k]);
+            ++ninv;
         }
-        if (k > 0) trsm(h, true, Lf[k].d(), dinv[k], int(a), src, cols, out.C[k], cols, int(cols));
-        else if (k + 1 == d) XRS_HIP(hipMemcpyAsync(out.C[k], src, t.size(k) * 8, hipMemcpyDeviceToDevice, h->stream));
     }
-    fork.join();
+    for (int b0 = 0; b0 < ninv; b0 += kTrinvBatchMax) {
+        TrinvBatch part{};
+        const int c = std::min(kTrinvBatchMax, ninv - b0);
+        for (int i = 0; i < c; ++i) {
+            part.L[i] = tb.L[b0 + i];
+            part.Dinv[i] = tb.Dinv[b0 + i];
+            part.X[i] = tb.X[b0 + i];
+            part.n[i] = tb.n[b0 + i];
+        }
+        trinv_batched(h, part, c);
+    }
+    std::vector<GemmJob> right, left;
+    for (size_t k = 0; k + 1 < d; ++k) {   // right factors: M_k (I (x) L_{k+1}), (r_k n_k) x r_{k+1} x r_{k+1}
+        const size_t b = t.r[k + 1];
+        right.push_back({t.rows_left(k), b, b, b, b, false, false, t.core[k], Lf[k + 1].d(), k == 0 ? out.C[k] : W[k].d()});
+    }
+    for (size_t k = 1; k < d; ++k) {       // left factors: Z_k (r_k x r_k) times the r_k x (n_k r_{k+1}) unfolding
+        const size_t a = t.r[k], cols = t.cols_right(k);
+        left.push_back({a, cols, a, a, cols, false, false, Z[k].d(), k + 1 < d ? W[k].d() : t.core[k], out.C[k]});
+    }
+    gemm_grouped(h, right);
+    gemm_grouped(h, left);
+    XRS_MARK("transforms");
 }
 
 // True when every factorisation of the pass succeeded (valid after the stream has been synchronised).
@@ -440,26 +519,20 @@ bool chain_status_ok(const ChainPass& p) {
 double chain_check(TT& t, const std::vector<double*>& C) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
+    XRS_MARK("check");
     std::vector<DevBuf> Gr(d);
     DevIdArgs da{};
     DevBuf dev(h, d * 16 * 8 + 64);
     int nchk = 0;
     for (size_t k = 1; k < d; ++k) Gr[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
-    if (t.sharded()) {   // the all-reduce hook synchronises the stream: stay on it
-        for (size_t k = 1; k < d; ++k) {
-            const size_t a = t.r[k], cols = t.cols_right(k);
-            gemm(h, Gr[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
-            t.reduce(Gr[k].d(), a * a);
-        }
-    } else {
-        StreamFork fork(h, xrs_handle_s::kSides);
-        for (size_t k = 1; k < d; ++k) {
-            fork.lane(int(k % size_t(fork.lanes())));
-            const size_t a = t.r[k], cols = t.cols_right(k);
-            gemm(h, Gr[k].d(), a, a, 1.0, C[k], cols, false, cols, C[k], cols, true);
-        }
-        fork.join();
+    std::vector<GemmJob> grams;
+    for (size_t k = 1; k < d; ++k) {
+        const size_t a = t.r[k], cols = t.cols_right(k);
+        grams.push_back({a, a, cols, cols, cols, false, true, C[k], C[k], Gr[k].d()});
     }
+    gemm_grouped(h, grams);
+    if (t.sharded())   // complete the mode sums across ranks
+        for (size_t k = 1; k < d; ++k) t.reduce(Gr[k].d(), t.r[k] * t.r[k]);
     for (size_t k = 1; k < d; ++k) {
         da.G[nchk] = Gr[k].d();
         da.n[nchk] = int(t.r[k]);
@@ -471,7 +544,9 @@ double chain_check(TT& t, const std::vector<double*>& C) {
     check_launch("k_dev_identity_many");
     double* hd = static_cast<double*>(h->host_scratch) + 64;
     XRS_HIP(hipMemcpyAsync(hd, dev.d(), size_t(nchk) * kSlices * 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_MARK("enq");
     XRS_HIP(hipStreamSynchronize(h->stream));
+    XRS_MARK("sync");
     double worst = 0.0;
     for (int i = 0; i < nchk * kSlices; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
     return worst;
@@ -493,12 +568,14 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     if (!(eps < 0.25 * cX * cX)) return false;
     // factorisation statuses (<= 3*64 ints) in a region of the pinned scratch no other routine uses
     int* hs = static_cast<int*>(t.h->host_scratch) + 12288;
+    HostMarks marks;
+    g_marks = marks.on ? &marks : nullptr;
     ChainPass p1;
     chain_pass(t, true, p1, hs);
     double dev = chain_check(t, p1.C);
     if (!chain_status_ok(p1)) {
         for (size_t k = 0; k < d; ++k) t.release(p1.C[k]);
-        return false;
+        { g_marks = nullptr; return false; }
     }
     std::vector<double*> C = p1.C;
     if (!(dev <= kOrthTol)) {
@@ -521,10 +598,11 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     const bool ok = dev <= kOrthTol;
     if (!ok && t.sharded()) {   // no sharded sequential sweep: report, cores untouched
         for (size_t k = 0; k < d; ++k) t.release(C[k]);
-        return false;
+        { g_marks = nullptr; return false; }
     }
     for (size_t k = 0; k < d; ++k) t.replace(k, C[k]);
     if (!ok) rl_sweep(t, max_ranks, eps, cX, d - 1);
+    g_marks = nullptr;
     return true;
 }
 
@@ -565,6 +643,46 @@ void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, 
     for (size_t k = d - 1; k >= 1; --k) truncate_edge(t, k, max_ranks[k - 1], eps);
 }
 
+// <x, y> with the zipper run from both ends at once (left environments on a side stream, right ones on
+// the main stream) and closed at the middle edge m by sum_ab E_m[a,b] F_m[a,b]: the two chains are
+// independent, so the critical path halves and the two streams fill the chip together.
+//   left  E_{k+1} (rx_{k+1} x ry_{k+1}) = sum_i X_k[:,i,:]^T E_k Y_k[:,i,:]      (E_0 = 1)
+//   right F_k     (rx_k x ry_k)         = sum_i X_k[:,i,:] F_{k+1} Y_k[:,i,:]^T  (F_d = 1)
+double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+                     const double* const* Y) {
+    const size_t m = d / 2;
+    size_t emax = 1, tmax = 1;
+    for (size_t k = 0; k <= d; ++k) emax = std::max(emax, rx[k] * ry[k]);
+    for (size_t k = 0; k < d; ++k) tmax = std::max(tmax, std::max(ry[k] * n[k] * rx[k + 1], rx[k] * n[k] * ry[k + 1]));
+    DevBuf E0(h, emax * 8), E1(h, emax * 8), F0(h, emax * 8), F1(h, emax * 8), TL(h, tmax * 8), TR(h, tmax * 8);
+    const double ones[2] = {1.0, 1.0};
+    XRS_HIP(hipMemcpyAsync(E0.d(), &ones[0], 8, hipMemcpyHostToDevice, h->stream));
+    XRS_HIP(hipMemcpyAsync(F0.d(), &ones[1], 8, hipMemcpyHostToDevice, h->stream));
+    double *E = E0.d(), *En = E1.d(), *F = F0.d(), *Fn = F1.d();
+    {
+        StreamFork fork(h);
+        const size_t steps = std::max(m, d - m);
+        for (size_t s = 0; s < steps; ++s) {   // launches interleaved step by step (see gram_chains)
+            if (s < m) {
+                fork.side();
+                const size_t k = s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+                gemm(h, TL.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);    // E^T X_k: b x (nk a2)
+                gemm(h, En, a2, b2, 1.0, TL.d(), a2, true, b * nk, Y[k], b2, false);       // ((b nk) x a2)^T Y_k
+                std::swap(E, En);
+            }
+            if (s < d - m) {
+                fork.main();
+                const size_t k = d - 1 - s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+                gemm(h, TR.d(), a * nk, b2, 1.0, X[k], a2, false, a2, F, b2, false);       // X_k F: (a nk) x b2
+                gemm(h, Fn, a, b, 1.0, TR.d(), nk * b2, false, nk * b2, Y[k], nk * b2, true);   // T Y_k^T: a x b
+                std::swap(F, Fn);
+            }
+        }
+        fork.join();
+    }
+    return reduce_to_host(h, 1, E, F, rx[m] * ry[m]);
+}
+
 double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
            const double* const* Y, const TT* shard = nullptr) {
     size_t emax = 1, tmax = 1;
@@ -572,6 +690,7 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
         emax = std::max(emax, rx[k + 1] * ry[k + 1]);
         tmax = std::max(tmax, ry[k] * n[k] * rx[k + 1]);
     }
+    if (!shard && d >= 4) return dot_two_ended(h, d, n, rx, X, ry, Y);
     DevBuf E0(h, emax * 8), E1(h, emax * 8), T(h, tmax * 8);
     const double one = 1.0;
     XRS_HIP(hipMemcpyAsync(E0.d(), &one, 8, hipMemcpyHostToDevice, h->stream));
