@@ -88,6 +88,13 @@ int xrs_gemm(xrs_handle_t handle, double* C, size_t M, size_t N, double alpha,
              const double* A, size_t lda, int transA, size_t K,
              const double* B, size_t ldb, int transB);
 
+/** Extension (no reference counterpart): `count` independent same-shape GEMMs
+ *  C[i] = alpha * op(A[i]) * op(B[i]) in one launch per 32 entries. A, B, C: host arrays of device
+ *  pointers; shapes and flags as in xrs_gemm. Used for the independent per-core products of a TT round. */
+int xrs_gemm_batched(xrs_handle_t handle, size_t count, double* const* C, size_t M, size_t N, double alpha,
+                     const double* const* A, size_t lda, int transA, size_t K,
+                     const double* const* B, size_t ldb, int transB);
+
 /* ---------------------------------------------------------------- permutation (tensor.h:65) */
 /** out = reshuffle(in, shuffle): out[...] with mode i of `in` moved to position shuffle[i]
  *  (indexedTensor_tensor_evaluate.cpp:55-143; shuffle[i] = NEW position of OLD mode i, :80-82).

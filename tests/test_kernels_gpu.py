@@ -68,6 +68,38 @@ def test_gemm_fp64(handle, ref, M, N, K, ta, tb):
     assert err <= 1e-13, err  # fp64 MFMA: relative Frobenius error at rounding level
 
 
+BATCHED = [
+    (9, 256, 256, 5120, False, True),    # chain-round check Grams (split-K, in-launch combine)
+    (7, 5120, 256, 256, False, False),   # right-factor transforms
+    (7, 256, 5120, 256, False, False),   # left-factor transforms
+    (3, 256, 256, 5120, True, False),
+    (5, 33, 65, 700, True, True),        # ragged tiles
+    (40, 64, 64, 64, False, False),      # more entries than one launch holds (32)
+    (1, 17, 19, 23, False, False),
+]
+
+
+@pytest.mark.parametrize("cnt,M,N,K,ta,tb", BATCHED)
+def test_gemm_batched_fp64(handle, ref, cnt, M, N, K, ta, tb):
+    """xrs_gemm_batched: every entry matches the GEMM oracle and the single-GEMM path (tile choice may differ)."""
+    rng = np.random.default_rng(cnt * 1000 + M + N + K)
+    As = [rng.standard_normal((K, M) if ta else (M, K)) for _ in range(cnt)]
+    Bs = [rng.standard_normal((N, K) if tb else (K, N)) for _ in range(cnt)]
+    dA = [handle.array(a) for a in As]
+    dB = [handle.array(b) for b in Bs]
+    dC = [handle.empty((M, N)) for _ in range(cnt)]
+    lda = M if ta else K
+    ldb = K if tb else N
+    handle.gemm_batched(dC, M, N, 0.5, dA, lda, ta, K, dB, ldb, tb)
+    for i in range(cnt):
+        got = dC[i].numpy()
+        expect = ref.gemm(As[i], ta, Bs[i], tb, 0.5)
+        err = np.linalg.norm(got - expect) / max(np.linalg.norm(expect), 1e-300)
+        assert err <= 1e-13, (i, err)
+    single = handle.matmul(dA[0], ta, dB[0], tb, 0.5).numpy()
+    assert np.linalg.norm(single - dC[0].numpy()) <= 1e-13 * np.linalg.norm(single)
+
+
 def test_gemm_zero_k(handle):
     dA, dB = handle.array(np.zeros((3, 0))), handle.array(np.zeros((0, 4)))
     out = handle.empty((3, 4))

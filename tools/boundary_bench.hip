@@ -76,6 +76,42 @@ int main() {
         CK(hipGraphDestroy(g1));
         CK(hipGraphDestroy(g2));
     }
+    // cross-stream hop: kernel on s0, event, s1 waits and runs a kernel, event, s0 waits, ...
+    {
+        hipStream_t s1;
+        CK(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+        hipEvent_t ev[2];
+        CK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+        const int hops = 100;
+        auto pingpong = [&] {
+            for (int i = 0; i < hops; ++i) {
+                hipStream_t a = (i & 1) ? s1 : st, b = (i & 1) ? st : s1;
+                hipLaunchKernelGGL(k_tiny, dim3(1), dim3(64), 0, a, p);
+                CK(hipEventRecord(ev[i & 1], a));
+                CK(hipStreamWaitEvent(b, ev[i & 1], 0));
+            }
+        };
+        const double t_ev = time_us(st, 10, pingpong) / hops;
+        // same chain with hipStreamWriteValue32 / hipStreamWaitValue32 on a device flag
+        unsigned* flag;
+        CK(hipMalloc(&flag, 64));
+        CK(hipMemset(flag, 0, 64));
+        unsigned epoch = 0;
+        auto pingpong_val = [&] {
+            for (int i = 0; i < hops; ++i) {
+                hipStream_t a = (i & 1) ? s1 : st, b = (i & 1) ? st : s1;
+                hipLaunchKernelGGL(k_tiny, dim3(1), dim3(64), 0, a, p);
+                ++epoch;
+                CK(hipStreamWriteValue32(a, flag, epoch, 0));
+                CK(hipStreamWaitValue32(b, flag, epoch, hipStreamWaitValueGte, 0xffffffffu));
+            }
+        };
+        const double t_val = time_us(st, 10, pingpong_val) / hops;
+        std::printf("cross-stream hop (tiny kernel + dependency): events %.2f us, write/wait value %.2f us\n", t_ev, t_val);
+        CK(hipStreamSynchronize(s1));
+        CK(hipFree(flag));
+    }
     CK(hipFree(p));
     return 0;
 }

@@ -41,6 +41,8 @@ SIGNATURES = {
     "xrs_axpy": (C.c_int, [_DP, _DP, C.c_double, _DP, _SZ]),
     "xrs_scale_rows": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ]),
     "xrs_gemm": (C.c_int, [_DP, _DP, _SZ, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
+    "xrs_gemm_batched": (C.c_int, [_DP, _SZ, C.POINTER(_DP), _SZ, _SZ, C.c_double, C.POINTER(_DP), _SZ, C.c_int, _SZ,
+                                   C.POINTER(_DP), _SZ, C.c_int]),
     "xrs_permute": (C.c_int, [_DP, _DP, _DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
     "xrs_qc": (C.c_int, [_DP, _DP, _DP, C.POINTER(_SZ), _DP, _SZ, _SZ]),
     "xrs_cq": (C.c_int, [_DP, _DP, _DP, C.POINTER(_SZ), _DP, _SZ, _SZ]),
@@ -153,6 +155,13 @@ class Handle:
     def gemm(self, C_: "DeviceArray", M, N, alpha, A: "DeviceArray", lda, transA, K, B: "DeviceArray", ldb, transB):
         _check("xrs_gemm", self.lib.xrs_gemm(self.h, _DP(C_.ptr), M, N, alpha, _DP(A.ptr), lda, int(transA), K,
                                             _DP(B.ptr), ldb, int(transB)))
+
+    def gemm_batched(self, Cs, M, N, alpha, As, lda, transA, K, Bs, ldb, transB):
+        """xrs_gemm_batched over lists of DeviceArrays (same shapes)."""
+        cnt = len(Cs)
+        tab = lambda xs: (_DP * max(1, cnt))(*[_DP(x.ptr) for x in xs])  # noqa: E731
+        _check("xrs_gemm_batched", self.lib.xrs_gemm_batched(self.h, cnt, tab(Cs), M, N, alpha, tab(As), lda, int(transA),
+                                                            K, tab(Bs), ldb, int(transB)))
 
     def matmul(self, A: "DeviceArray", transA: bool, B: "DeviceArray", transB: bool, alpha: float = 1.0):
         """Row-major C = alpha*op(A)*op(B) with the reference's inline-overload ld convention."""

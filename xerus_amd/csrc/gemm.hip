@@ -390,10 +390,12 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         else if (ntiles(64, 32) >= 256) var = 3;   // 32x32 is 2 us faster alone but 2x the workgroups:
         else if (ntiles(32, 32) >= 512) var = 4;   // it starves the concurrent latency-bound TRSMs
         else {
+            static const bool prefer_inlaunch = std::getenv("XRS_GEMM_PREFER_INLAUNCH") != nullptr;
             var = 4;
             for (int v : {1, 2, 3}) {
                 const long t = ntiles(bms[v], bns[v]);
                 const long sp = std::min<long>((cfg_target + t - 1) / t, std::max<long>(1, K / cfg_kmin));
+                if (prefer_inlaunch && sp * bms[v] * bns[v] * 8 > 65536) continue;
                 if (t * sp >= cfg_target) { var = v; break; }
             }
         }
@@ -417,7 +419,11 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     static const bool two_kernel = std::getenv("XRS_GEMM_SPLITK2") != nullptr;
     // The last arriver reads splits x BM x BN doubles serially: worth it for small tiles only (the guide's
     // "a few tens of KB" per tile; 128x128 tiles at 2 splits measured 70 us slower than the reduce kernel).
-    const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= 65536;
+    static const size_t slab_cap = [] {
+        const char* e = std::getenv("XRS_GEMM_SLAB_CAP");   // bytes per tile (tuning experiments)
+        return e ? size_t(std::atoll(e)) : size_t(65536);
+    }();
+    const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= slab_cap && bms[var] * bns[var] <= 4096;
     int* tickets = (splits > 1 && !two_kernel && small_slab && ntiles(bms[var], bns[var]) <= xrs_handle_s::kTicketCap)
                        ? h->tickets : nullptr;
 #define XRS_TILES(...) launch_tiles<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets)
@@ -484,5 +490,23 @@ extern "C" int xrs_gemm(xrs_handle_t h, double* C, size_t M, size_t N, double al
         XRS_REQUIRE(transB ? ldb >= K || N == 0 : ldb >= N || K == 0, "ldb too small");
         XRS_REQUIRE(C != A && C != B, "C must not alias A or B");
         xrs::gemm(h, C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
+    });
+}
+
+extern "C" int xrs_gemm_batched(xrs_handle_t h, size_t count, double* const* C, size_t M, size_t N, double alpha,
+                                const double* const* A, size_t lda, int transA, size_t K, const double* const* B,
+                                size_t ldb, int transB) {
+    return xrs::guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        XRS_REQUIRE(count == 0 || (A && B && C), "null pointer table");
+        XRS_REQUIRE(count < (1u << 20), "batch too large");
+        XRS_REQUIRE(transA ? lda >= M || K == 0 : lda >= K || M == 0, "lda too small");
+        XRS_REQUIRE(transB ? ldb >= K || N == 0 : ldb >= N || K == 0, "ldb too small");
+        for (size_t i = 0; i < count; ++i) {
+            XRS_REQUIRE(M == 0 || N == 0 || C[i], "null C");
+            XRS_REQUIRE(K == 0 || M == 0 || N == 0 || (A[i] && B[i]), "null A/B");
+            XRS_REQUIRE(C[i] != A[i] && C[i] != B[i], "C must not alias A or B");
+        }
+        xrs::gemm_batched(h, int(count), C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
     });
 }

@@ -94,6 +94,10 @@ struct xrs_handle_s {
     xrs::Pool* side_pool[kSides] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kSides] = {};
     hipEvent_t ev_aux = nullptr;   // one extra cross-stream dependency inside a fork (see tt.hip chain_pass)
+    // fork/join words for stream write-value / wait-value dependencies (one 64-byte line each: main, sides);
+    // epochs only grow (waits are >=)
+    unsigned* sync_words = nullptr;
+    unsigned sync_epoch[1 + kSides] = {};
     // split-K arrival tickets (zero between launches; the last arriving slice resets its word), one
     // array per stream so concurrent launches never share a word; `tickets` follows `stream`
     static constexpr int kTicketCap = 4096;
