@@ -523,10 +523,221 @@ __device__ __forceinline__ void potrf_rr_body(double* __restrict__ G, int n, dou
     if (tid == 0) status[0] = fail;
 }
 
-__global__ void __launch_bounds__(PR_THREADS) k_potrf_rr(double* __restrict__ G, int n, double shift_rel,
+// ---------------------------------------------------------------------------------------------
+// Lookahead variant of the register-resident Cholesky (n <= 256). Wave 0 factors the diagonal blocks
+// and owns only the tiles of the first column (plus (1,1)), which receive no trailing update after
+// step 0; the other tiles live on waves 1..7 (17 slots each, the plain kernel's register footprint).
+// Step j:
+//   (C_j)  owners of the panel tiles (i, j) form L_ij = G_ij L_jj^{-T} and publish them;
+//   (D1_j) owners of column j+1 apply the rank-16 update of panel j to it; the owner of (j+1, j+1)
+//          publishes it;
+//   (B_{j+1} || D2_j) wave 0 factors block j+1 while waves 1..7 update the rest of the trailing matrix.
+// The diagonal chain (42 % of the plain kernel) thus runs beside the trailing update.
+constexpr int LA_THREADS = PR_THREADS;
+constexpr int LA_WAVES = LA_THREADS / 64;
+constexpr int LA_SLOTS = PR_SLOTS;   // wave 0: tiles 0..16 (column 0 and tile (1,1), final after step 0);
+                                     // waves 1..7: tile 17 + 7 s + (wave - 1)
+
+// slots P, P-1 with kmin <= tk <= kmax: G_ik -= L_ij L_kj^T (interleaved MFMA chains; inactive -> no-op)
+template <int P>
+__device__ __forceinline__ void la_trail_pair(d4 (&acc)[LA_SLOTS], const int (&ti)[LA_SLOTS], const int (&tk)[LA_SLOTS],
+                                              int kmin, int kmax, const double* Pbuf, int oa) {
+    const bool hi = tk[P] >= kmin && tk[P] <= kmax;
+    bool lo = false;
+    if constexpr (P > 0) lo = tk[P - 1] >= kmin && tk[P - 1] <= kmax;
+    if (!hi && !lo) return;
+    auto op = [&](int tile, int c) -> double {
+        return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(Pbuf + max(tile, 0) * PTILE) + oa + 32 * c);
+    };
+    double a1[4], b1[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        a1[c] = hi ? -op(ti[P], c) : 0.0;
+        b1[c] = hi ? op(tk[P], c) : 0.0;
+    }
+    if constexpr (P > 0) {
+        double a0[4], b0[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            a0[c] = lo ? -op(ti[P - 1], c) : 0.0;
+            b0[c] = lo ? op(tk[P - 1], c) : 0.0;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            acc[P] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[c], b1[c], acc[P], 0, 0, 0);
+            acc[P - 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[c], b0[c], acc[P - 1], 0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[P] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[c], b1[c], acc[P], 0, 0, 0);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void la_trail_all(d4 (&acc)[LA_SLOTS], const int (&ti)[LA_SLOTS], const int (&tk)[LA_SLOTS],
+                                             int kmin, int kmax, const double* Pbuf, int oa) {
+    if constexpr (P >= 0) {
+        la_trail_pair<P>(acc, ti, tk, kmin, kmax, Pbuf, oa);
+        la_trail_all<P - 2>(acc, ti, tk, kmin, kmax, Pbuf, oa);
+    }
+}
+
+__device__ __forceinline__ void potrf_la_body(double* __restrict__ G, int n, double shift_rel, double* __restrict__ Dinv,
+                                              int* __restrict__ status, double* __restrict__ info,
+                                              const double* __restrict__ src = nullptr) {
+    const double* __restrict__ S = src != nullptr ? src : G;
+    __shared__ double Dt[PTILE];
+    __shared__ double Di[PTILE];
+    __shared__ double P[PR_TMAX * PTILE];
+    __shared__ double ivs[16];
+    __shared__ double red[LA_WAVES];
+    __shared__ int fail;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 15, lg = lane >> 4;
+    const int T = (n + 15) >> 4;
+    const int ntiles = T * (T + 1) / 2;
+    if (tid == 0) fail = 0;
+    PSTAMP(0);
+    double tr = 0.0;
+    for (int i = tid; i < n; i += LA_THREADS) tr += S[size_t(i) * n + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
+    if (lane == 0) red[wave] = tr;
+    __syncthreads();
+    tr = 0.0;
+#pragma unroll
+    for (int w = 0; w < LA_WAVES; ++w) tr += red[w];
+    if (tid == 0 && info) info[0] = tr;
+    const double shift = shift_rel * tr;
+
+    // tile ownership + load (identity padding beyond n)
+    int ti[LA_SLOTS], tk[LA_SLOTS];
+    d4 acc[LA_SLOTS];
+#pragma unroll
+    for (int s = 0; s < LA_SLOTS; ++s) {
+        const int t = wave == 0 ? s : LA_SLOTS + s * (LA_WAVES - 1) + (wave - 1);
+        int i = -1, k = -1;
+        if (t < ntiles) {
+            int start = 0;
+            k = 0;
+            while (t >= start + (T - k)) { start += T - k; ++k; }
+            i = k + (t - start);
+        }
+        ti[s] = i;
+        tk[s] = k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = min(max(16 * i + lg + 4 * q, 0), n - 1), col = min(max(16 * k + lr, 0), n - 1);
+            acc[s][q] = S[size_t(row) * n + col];
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < LA_SLOTS; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 16 * ti[s] + lg + 4 * q, col = 16 * tk[s] + lr;
+            const bool inside = ti[s] >= 0 && row < n && col < n;
+            const double pad = (row == col) ? 1.0 : 0.0;
+            acc[s][q] = inside ? acc[s][q] + ((row == col) ? shift : 0.0) : pad;
+        }
+
+    int oc = (lg * PT + lr) * 8, oa = (lr * PT + lg) * 8;
+    auto cpos = [&](double* base, int q) -> double* {   // C layout (row lg + 4q, col lr)
+        return reinterpret_cast<double*>(reinterpret_cast<char*>(base) + oc) + 4 * q * PT;
+    };
+    auto apos = [&](const double* base, int c) -> const double* {   // A/B operand (row lr, k 4c + lg)
+        return reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + oa) + 4 * c;
+    };
+    auto publish_diag = [&](int j) {   // owner of (j, j) -> Dt
+#pragma unroll
+        for (int s = 0; s < LA_SLOTS; ++s)
+            if (ti[s] == j && tk[s] == j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) *cpos(Dt, q) = acc[s][q];
+            }
+    };
+    auto factor_diag = [&](int j) {   // wave 0: Dt -> L_jj (Dt), L_jj^{-1} (Di, Dinv)
+        if (wave == 0) {
+            const int bad = diag_factor16(Dt, Di, ivs, Dinv + size_t(j) * 256, lane, n - 16 * j);
+            if (lane == 0 && bad && fail == 0) fail = 16 * j + bad;
+        }
+    };
+    publish_diag(0);
+    __syncthreads();
+    factor_diag(0);
+    __syncthreads();
+    for (int j = 0; j < T; ++j) {
+        // opaque lane offsets per iteration (keeps LICM from hoisting per-slot LDS addresses -> spills)
+        asm volatile("" : "+v"(oc), "+v"(oa));
+        PSTAMP(2 + 4 * j);
+        // (C_j) panel
+#pragma unroll
+        for (int s = 0; s < LA_SLOTS; ++s) {
+            if (tk[s] != j) continue;
+            if (ti[s] == j) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[s][q] = *cpos(Dt, q);
+                continue;
+            }
+            double* Pi = P + ti[s] * PTILE;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *cpos(Pi, q) = acc[s][q];
+            wave_lds_sync();
+            d4 rr = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) rr = __builtin_amdgcn_mfma_f64_16x16x4f64(*apos(Pi, c), *apos(Di, c), rr, 0, 0, 0);
+            wave_lds_sync();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *cpos(Pi, q) = rr[q];
+            acc[s] = rr;
+        }
+        __syncthreads();
+        if (j + 1 >= T) break;
+        PSTAMP(3 + 4 * j);
+        // (D1_j) column j+1 first, then publish the new diagonal block
+        la_trail_all<LA_SLOTS - 1>(acc, ti, tk, j + 1, j + 1, P, oa);
+        publish_diag(j + 1);
+        __syncthreads();
+        PSTAMP(4 + 4 * j);
+        // (B_{j+1} || D2_j); wave 0 factors first, then updates whatever trailing tiles it owns (none
+        // for n = 256 after step 0)
+        if (wave == 0) factor_diag(j + 1);
+        la_trail_all<LA_SLOTS - 1>(acc, ti, tk, j + 2, T - 1, P, oa);
+        __syncthreads();
+    }
+    PSTAMP(1);
+    int sg = lg, sr = lr;
+    asm volatile("" : "+v"(sg), "+v"(sr));
+#pragma unroll
+    for (int s = 0; s < LA_SLOTS; ++s) {
+        if (ti[s] < 0 || G == nullptr) continue;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int row = 16 * ti[s] + sg + 4 * q, col = 16 * tk[s] + sr;
+            if (row < n && col < n) {
+                G[size_t(row) * n + col] = (col <= row) ? acc[s][q] : 0.0;
+                if (ti[s] != tk[s]) G[size_t(col) * n + row] = 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) status[0] = fail;
+}
+
+// The lookahead body (n = 256: 150.6 vs 158.8 us per factorisation; n = 100: 64 vs 54 us — one kernel
+// holding both bodies spills, so the lookahead one serves every n <= 256). -DXRS_POTRF_NO_LOOKAHEAD
+// builds the plain body (A/B timing, tools/potrf_bench.hip).
+#ifdef XRS_POTRF_NO_LOOKAHEAD
+#define XRS_POTRF_RR_BODY potrf_rr_body
+#else
+#define XRS_POTRF_RR_BODY potrf_la_body
+#endif
+#define XRS_POTRF_RR_THREADS PR_THREADS
+__global__ void __launch_bounds__(XRS_POTRF_RR_THREADS) k_potrf_rr(double* __restrict__ G, int n, double shift_rel,
                                                          double* __restrict__ Dinv, int* __restrict__ status,
                                                          double* __restrict__ info) {
-    potrf_rr_body(G, n, shift_rel, Dinv, status, info);
+    XRS_POTRF_RR_BODY(G, n, shift_rel, Dinv, status, info);
 }
 
 // Independent factorisations, one workgroup each (e.g. the Gram matrices of every TT edge).
@@ -535,9 +746,9 @@ __global__ void __launch_bounds__(POT_THREADS) k_potrf32_batched(PotrfBatch b) {
     potrf32_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
 }
 
-__global__ void __launch_bounds__(PR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
+__global__ void __launch_bounds__(XRS_POTRF_RR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
     const int i = blockIdx.x;
-    potrf_rr_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
+    XRS_POTRF_RR_BODY(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -978,7 +1189,7 @@ void potrf(xrs_handle_t h, double* G, int n, double shift_rel, double* Dinv, int
     XRS_REQUIRE(n >= 1 && n <= PMAX, "potrf: n out of range for the single-workgroup kernel");
     KernelTimer timer(h, XRS_KFAM_QR, double(n) * n * n / 3.0, 16.0 * double(n) * n);
     if (dinv_ld(n) == 16) {
-        hipLaunchKernelGGL(k_potrf_rr, dim3(1), dim3(PR_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
+        hipLaunchKernelGGL(k_potrf_rr, dim3(1), dim3(XRS_POTRF_RR_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
         check_launch("k_potrf_rr");
     } else {
         hipLaunchKernelGGL(k_potrf, dim3(1), dim3(POT_THREADS), 0, h->stream, G, n, shift_rel, Dinv, status_dev, info_dev);
@@ -1014,7 +1225,7 @@ void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count) {
     large.status = st.as<int>() + ns;
     if (ns) {
         KernelTimer timer(h, XRS_KFAM_QR, fl_s, 0.0);
-        hipLaunchKernelGGL(k_potrf_rr_batched, dim3(ns), dim3(PR_THREADS), 0, h->stream, small);
+        hipLaunchKernelGGL(k_potrf_rr_batched, dim3(ns), dim3(XRS_POTRF_RR_THREADS), 0, h->stream, small);
         check_launch("k_potrf_rr_batched");
     }
     if (nl) {
