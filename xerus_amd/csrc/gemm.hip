@@ -42,8 +42,13 @@ struct GemmMany {
     __device__ double* c(int i) const { return C[i]; }
 };
 
+// Occupancy hint: the second __launch_bounds__ argument is the minimum number of waves per SIMD. Two
+// 8-wave workgroups per CU need 4 (a 128-VGPR budget); the 128x128 tile keeps 2 (256 VGPRs, 1 per CU).
+template <int BM, int BN, int WGM, int WGN, int WGK>
+constexpr int gemm_min_waves() { return (BM * BN >= 128 * 128) ? 2 : 4; }
+
 template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB, class PTR>
-__global__ void __launch_bounds__(WGM * WGN * WGK * 64, (WGM * WGN * WGK * 64 * 2 <= 1024) ? 2 : 1)
+__global__ void __launch_bounds__(WGM * WGN * WGK * 64, (gemm_min_waves<BM, BN, WGM, WGN, WGK>()))
 k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
            double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets) {
     const int bz = blockIdx.y;   // batch entry
@@ -54,8 +59,10 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
     const int tslot = bz * int(gridDim.x) + int(blockIdx.x);    // this tile's ticket
     constexpr int NT = WGM * WGN * WGK * 64;   // WGK wave groups split every K-step's MFMA k-substeps
     // LDS rows of BM / BN doubles, XOR-swizzled per k row: element (k, m) at k*SA + (m ^ swz(k)) with
-    // swz(k) = 16*(k&1) + (k>>1). Fragment reads (lanes: 16 m x rows k, k+1) hit 32 distinct bank pairs
-    // and the transposed stores (lanes: 16 consecutive k, one m) 16 distinct ones.
+    // swz(k) = 16*(k&1) | (k&15). ds_read_b64 banks over 32-lane groups, (a/4) mod 64: the fragment reads
+    // (16 m x rows k, k+1) cover all 32 8-byte bank pairs; ds_write_b64 banks over 16-lane groups,
+    // (a/4) mod 32: the transposed stores (16 consecutive k, one m) get 16 distinct low nibbles (the
+    // former (k>>1) swizzle paired them: SQ_LDS_BANK_CONFLICT ~1 cycle per LDS instruction).
     constexpr int SA = BM;
     constexpr int SB = BN;
     static_assert(BM % 32 == 0 && BN % 32 == 0, "swizzle needs 32-aligned tile rows");
@@ -112,7 +119,7 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc2[a][i][j] = d4{0.0, 0.0, 0.0, 0.0};
-    auto swz = [](int k) { return ((k & 1) << 4) | ((k >> 1) & 15); };
+    auto swz = [](int k) { return ((k & 1) << 4) | (k & 15); };
 
     // register ring: the global loads of K-step t+PD are issued while step t computes, so PD steps of
     // MFMA work cover the global-memory latency (one step is only ~4-8 MFMAs per wave)
@@ -153,14 +160,16 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
             int m, k;
             a_coord(e, m, k);
             const bool ok = (m0 + m < M) && (k0 + k < kend);
-            if (tid + e * NT < BM * GBK) As[buf][k * SA + (m ^ swz(k))] = ok ? ra[slot][e] : 0.0;
+            // (no guard when the tile divides evenly over the threads: a branch here makes the waitcnt
+            // pass lose track of the ring's loads and drain vmcnt(0) at the loop head)
+            if ((BM * GBK) % NT == 0 || tid + e * NT < BM * GBK) As[buf][k * SA + (m ^ swz(k))] = ok ? ra[slot][e] : 0.0;
         }
 #pragma unroll
         for (int e = 0; e < B_PER; ++e) {
             int n, k;
             b_coord(e, n, k);
             const bool ok = (n0 + n < N) && (k0 + k < kend);
-            if (tid + e * NT < BN * GBK) Bs[buf][k * SB + (n ^ swz(k))] = ok ? rb[slot][e] : 0.0;
+            if ((BN * GBK) % NT == 0 || tid + e * NT < BN * GBK) Bs[buf][k * SB + (n ^ swz(k))] = ok ? rb[slot][e] : 0.0;
         }
     };
     const int lr = lane & 15, lk = lane >> 4;
@@ -186,8 +195,10 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
     const int nsteps = (kend > kbeg) ? (kend - kbeg + GBK - 1) / GBK : 0;
     if (nsteps > 0) {
         static_assert(PD % 2 == 0, "ring depth must be even (LDS double buffer parity)");
+        // unconditional (clamped addresses; slots past the slice end are never stored): branch-free, so
+        // the waitcnt pass can count the ring
         [&]<int... U>(std::integer_sequence<int, U...>) {
-            ((U < nsteps ? load_tile(kbeg + U * GBK, std::integral_constant<int, U>{}) : void()), ...);
+            (load_tile(kbeg + U * GBK, std::integral_constant<int, U>{}), ...);
         }(std::make_integer_sequence<int, PD>{});
         store_tile(0, kbeg, std::integral_constant<int, 0>{});
         __syncthreads();
@@ -364,6 +375,7 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     //   v2  64x64  (8 waves 2x4)              mid-size
     //   v3  64x32  (8 waves 2x2, K split 2)   split-K Gram shapes (r x r, K = n r)
     //   v4  32x32  (8 waves 2x2, K split 2)   TT "wide"/"tall" shapes (M or N = r, other = n r)
+    //   v8/v9: v3/v4 with a 4-deep ring (tuning only)
     // split-K brings the grid to ~target workgroups while every split keeps >= kmin of K.
     static int cfg_var = 0, cfg_kmin = 256, cfg_target = 512;
     static bool cfg_read = false;
@@ -373,10 +385,11 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     }
     // (batched: the tile counts are over the whole batch)
     auto ntiles = [&](int bm, int bn) { return long(count) * ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    const int bms[8] = {0, 128, 64, 64, 32, 64, 64, 64}, bns[8] = {0, 128, 64, 32, 32, 32, 64, 64};
+    const int bms[10] = {0, 128, 64, 64, 32, 64, 64, 64, 64, 32}, bns[10] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32};
     int var = cfg_var;
     if (var == 0) {
-        // measured on the TT shapes (tools/gemm_tt_bench.py, profiles/r01/gemm_tt_sweep.txt):
+        // measured on the TT shapes (tools/gemm_tt_bench.py, profiles/r01/gemm_tt_sweep*.txt; the 32x32
+        // and 64x32 tiles use a 2-deep ring since the waitcnt fix: 24.6 vs 27.2 us on 256x5120x256):
         //   256 x 5120 x 256 wide/tall: 32x32 24.8 us < 64x32 26.8 < 64x64 28.6 < 128x128 44.5 (alone;
         //                               with 3 concurrent streams 64x32 wins, see below)
         //   512 x 10240 x 512:          64x64 131 us < 64x32 148 < 128x128 154
@@ -387,8 +400,9 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         // `target` workgroups (fewer, larger tiles re-read less of the long-K operands).
         if (ntiles(128, 128) >= 1000) var = 1;
         else if (ntiles(64, 64) >= 512) var = 2;
-        else if (ntiles(64, 32) >= 256) var = 3;   // 32x32 is 2 us faster alone but 2x the workgroups:
-        else if (ntiles(32, 32) >= 512) var = 4;   // it starves the concurrent latency-bound TRSMs
+        else if (ntiles(32, 32) >= 1024) var = 4;
+        else if (ntiles(64, 32) >= 256) var = 3;
+        else if (ntiles(32, 32) >= 512) var = 4;
         else {
             static const bool prefer_inlaunch = std::getenv("XRS_GEMM_PREFER_INLAUNCH") != nullptr;
             var = 4;
@@ -407,11 +421,11 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         const long maxs = std::max<long>(1, K / cfg_kmin);
         splits = int(std::max<long>(1, std::min(want, maxs)));
     }
-    const int bk = (var >= 5) ? 32 : 16;
+    const int bk = (var >= 5 && var <= 7) ? 32 : 16;
     int kps = (K + splits - 1) / splits;
     kps = (kps + bk - 1) / bk * bk;
     splits = (K + kps - 1) / kps;
-    if (std::is_same<PTR, GemmMany>::value && var >= 5) var = (var == 5) ? 3 : 2;   // tuning-only tiles: single GEMMs
+    if (std::is_same<PTR, GemmMany>::value && var >= 5) var = (var == 5 || var == 8) ? 3 : (var == 9 ? 4 : 2);   // tuning-only tiles: single GEMMs
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
     // one-launch split-K when the tile grid fits the stream's ticket array (XRS_GEMM_SPLITK2=1: old
@@ -430,11 +444,13 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     switch (var) {
         case 1: XRS_TILES(128, 128, 16, 2, 4, 1, 2); break;
         case 2: XRS_TILES(64, 64, 16, 2, 4, 1, 4); break;
-        case 3: XRS_TILES(64, 32, 16, 2, 2, 2, 4); break;
+        case 3: XRS_TILES(64, 32, 16, 2, 2, 2, 2); break;
         case 5: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 32, 32, 2, 2, 2, 4); break;
         case 6: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 64, 32, 2, 2, 1, 4); break;
         case 7: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 64, 32, 2, 2, 2, 4); break;
-        default: XRS_TILES(32, 32, 16, 2, 2, 2, 4); break;
+        case 8: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 32, 16, 2, 2, 2, 4); break;
+        case 9: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 16, 2, 2, 2, 4); break;
+        default: XRS_TILES(32, 32, 16, 2, 2, 2, 2); break;
     }
 #undef XRS_TILES
     if (splits > 1 && tickets == nullptr) {
