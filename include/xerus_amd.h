@@ -95,6 +95,13 @@ int xrs_gemm_batched(xrs_handle_t handle, size_t count, double* const* C, size_t
                      const double* const* A, size_t lda, int transA, size_t K,
                      const double* const* B, size_t ldb, int transB);
 
+/** Extension (no reference counterpart): C (N x N) = alpha * op(A) * op(B) for a product the caller
+ *  knows to be symmetric (a Gram A^T A, or M^T G M with G symmetric). Only the tiles on or below the
+ *  diagonal are computed; the result is written exactly symmetric. Flags and ld as in xrs_gemm (M = N). */
+int xrs_gemm_sym(xrs_handle_t handle, double* C, size_t N, double alpha,
+                 const double* A, size_t lda, int transA, size_t K,
+                 const double* B, size_t ldb, int transB);
+
 /* ---------------------------------------------------------------- permutation (tensor.h:65) */
 /** out = reshuffle(in, shuffle): out[...] with mode i of `in` moved to position shuffle[i]
  *  (indexedTensor_tensor_evaluate.cpp:55-143; shuffle[i] = NEW position of OLD mode i, :80-82).

@@ -100,6 +100,39 @@ def test_gemm_batched_fp64(handle, ref, cnt, M, N, K, ta, tb):
     assert np.linalg.norm(single - dC[0].numpy()) <= 1e-13 * np.linalg.norm(single)
 
 
+SYMS = [
+    (256, 5120, True, False),   # chain Gram M^T T (split-K, two-kernel reduce)
+    (256, 5120, False, True),   # right chain / check Gram M T^T
+    (20, 400, True, False),     # edge core
+    (100, 3000, False, True),   # ragged tiles across the diagonal
+    (512, 10240, False, True),  # cfg5
+    (33, 17, True, False),
+]
+
+
+@pytest.mark.parametrize("N,K,ta,tb", SYMS)
+def test_gemm_sym_fp64(handle, ref, N, K, ta, tb):
+    """xrs_gemm_sym on M^T G M / X X^T products: exactly symmetric, equal to the GEMM oracle."""
+    rng = np.random.default_rng(N + K)
+    X = rng.standard_normal((K, N) if ta else (N, K))
+    G = rng.standard_normal((K, K)) if K <= 1000 else None
+    if G is not None:   # B = G X (K x N) with G symmetric: op(A) op(B) = X^T (G_s X) is symmetric
+        Gs = G + G.T
+        A = X
+        B = (Gs @ X) if ta else (X @ Gs)
+    else:
+        A = B = X
+    dA, dB, dC = handle.array(A), handle.array(B), handle.empty((N, N))
+    lda = A.shape[1]
+    ldb = B.shape[1]
+    handle.gemm_sym(dC, N, 0.5, dA, lda, ta, K, dB, ldb, tb)
+    got = dC.numpy()
+    expect = ref.gemm(A, ta, B, tb, 0.5)
+    assert np.array_equal(got, got.T)
+    err = np.linalg.norm(got - expect) / np.linalg.norm(expect)
+    assert err <= 1e-13, err
+
+
 def test_gemm_zero_k(handle):
     dA, dB = handle.array(np.zeros((3, 0))), handle.array(np.zeros((0, 4)))
     out = handle.empty((3, 4))

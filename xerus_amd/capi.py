@@ -41,6 +41,7 @@ SIGNATURES = {
     "xrs_axpy": (C.c_int, [_DP, _DP, C.c_double, _DP, _SZ]),
     "xrs_scale_rows": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ]),
     "xrs_gemm": (C.c_int, [_DP, _DP, _SZ, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
+    "xrs_gemm_sym": (C.c_int, [_DP, _DP, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
     "xrs_gemm_batched": (C.c_int, [_DP, _SZ, C.POINTER(_DP), _SZ, _SZ, C.c_double, C.POINTER(_DP), _SZ, C.c_int, _SZ,
                                    C.POINTER(_DP), _SZ, C.c_int]),
     "xrs_permute": (C.c_int, [_DP, _DP, _DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
@@ -155,6 +156,10 @@ class Handle:
     def gemm(self, C_: "DeviceArray", M, N, alpha, A: "DeviceArray", lda, transA, K, B: "DeviceArray", ldb, transB):
         _check("xrs_gemm", self.lib.xrs_gemm(self.h, _DP(C_.ptr), M, N, alpha, _DP(A.ptr), lda, int(transA), K,
                                             _DP(B.ptr), ldb, int(transB)))
+
+    def gemm_sym(self, C_: "DeviceArray", N, alpha, A: "DeviceArray", lda, transA, K, B: "DeviceArray", ldb, transB):
+        _check("xrs_gemm_sym", self.lib.xrs_gemm_sym(self.h, _DP(C_.ptr), N, alpha, _DP(A.ptr), lda, int(transA), K,
+                                                    _DP(B.ptr), ldb, int(transB)))
 
     def gemm_batched(self, Cs, M, N, alpha, As, lda, transA, K, Bs, ldb, transB):
         """xrs_gemm_batched over lists of DeviceArrays (same shapes)."""

@@ -25,7 +25,11 @@ void gemm(xrs_handle_t h, double* C, size_t M, size_t N, double alpha, const dou
 // Batch of same-shape GEMMs C[i] = alpha op(A[i]) op(B[i]) in one launch per kGemmBatchMax entries
 constexpr int kGemmBatchMax = 32;
 void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t M, size_t N, double alpha, const double* const* A,
-                  size_t lda, bool ta, size_t K, const double* const* B, size_t ldb, bool tb);
+                  size_t lda, bool ta, size_t K, const double* const* B, size_t ldb, bool tb, bool sym = false);
+// C (N x N) = alpha op(A) op(B) for a product KNOWN to be symmetric (Grams, M^T G M with G symmetric):
+// only the lower tiles are computed and mirrored, so C is exactly symmetric
+void gemm_sym(xrs_handle_t h, double* C, size_t N, double alpha, const double* A, size_t lda, bool ta, size_t K,
+              const double* B, size_t ldb, bool tb);
 
 // permute.hip
 void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const size_t* dims, const size_t* shuffle);

@@ -50,7 +50,7 @@ constexpr int gemm_min_waves() { return (BM * BN >= 128 * 128) ? 2 : 4; }
 template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB, class PTR>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64, (gemm_min_waves<BM, BN, WGM, WGN, WGK>()))
 k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
-           double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets) {
+           double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym) {
     const int bz = blockIdx.y;   // batch entry
     const double* __restrict__ A = ptrs.a(bz);
     const double* __restrict__ B = ptrs.b(bz);
@@ -108,6 +108,10 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
             tn = b / tiles_m;
         }
     }
+    // symmetric result (sym, square tiles, M == N): only tiles on or below the diagonal are computed;
+    // each lower element is also written to its mirror position
+    if (sym && tm < tn) return;
+    const bool mirror = sym != 0;
     const int m0 = tm * BM, n0 = tn * BN;
     const int kbeg = blockIdx.z * kps;
     const int kend = min(K, kbeg + kps);
@@ -286,8 +290,12 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
                         if (tickets != nullptr)   // write-through (sc1): visible to any XCD without a release fence
                             __hip_atomic_store(&out[size_t(row) * N + col], acc[i][j][r], __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
-                        else
+                        else if (!mirror || to_slab)
                             out[size_t(row) * N + col] = scale * acc[i][j][r];
+                        else if (row >= col) {
+                            out[size_t(row) * N + col] = scale * acc[i][j][r];
+                            out[size_t(col) * N + row] = scale * acc[i][j][r];
+                        }
                     }
                 }
             }
@@ -316,7 +324,7 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int row = m0 + wm + i * 16 + lg + 4 * r;
-                if (row < M && col < N) {
+                if (row < M && col < N && (!mirror || row >= col)) {
                     const size_t o = size_t(row) * N + col;
                     double sum = 0.0;
                     for (int z = 0; z < int(gridDim.z); ++z)
@@ -324,6 +332,7 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
                                                       : __hip_atomic_load(&slab[(size_t(bz) * gridDim.z + z) * MN + o], __ATOMIC_RELAXED,
                                                                           __HIP_MEMORY_SCOPE_AGENT);
                     C[o] = alpha * sum;
+                    if (mirror) C[size_t(col) * N + row] = alpha * sum;
                 }
             }
         }
@@ -331,20 +340,27 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
 
 template <class PTR>
 __global__ void __launch_bounds__(256) k_splitk_reduce(const PTR ptrs, const double* __restrict__ slab, size_t MN,
-                                                       int splits, double alpha) {
+                                                       int splits, double alpha, int symN) {
     double* __restrict__ C = ptrs.c(blockIdx.y);
     slab += size_t(blockIdx.y) * splits * MN;
     const size_t stride = size_t(gridDim.x) * blockDim.x;
     for (size_t i = size_t(blockIdx.x) * blockDim.x + threadIdx.x; i < MN; i += stride) {
+        size_t row = 0, col = 0;
+        if (symN) {   // symmetric result: lower elements only (the upper slabs were never written)
+            row = i / size_t(symN);
+            col = i - row * size_t(symN);
+            if (col > row) continue;
+        }
         double s = 0.0;
         for (int z = 0; z < splits; ++z) s += slab[size_t(z) * MN + i];
         C[i] = alpha * s;
+        if (symN) C[col * size_t(symN) + row] = alpha * s;
     }
 }
 
 template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, class PTR>
 static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bool ta, size_t ldb, bool tb,
-                         int M, int N, int K, int splits, int kps, double alpha, double* slab, int* tickets) {
+                         int M, int N, int K, int splits, int kps, double alpha, double* slab, int* tickets, int sym) {
     const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     dim3 grid(unsigned(tiles_m * tiles_n), unsigned(count), unsigned(splits));
     // group by the larger operand's panels (B: K x N, A: M x K) when the tile grid allows a bijection
@@ -357,7 +373,7 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
                       count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GEMM_LAUNCH(TA_, TB_)                                                                             \
     hipLaunchKernelGGL((k_gemm_f64<BM, BN, GBK, WGM, WGN, WGK, PD, TA_, TB_, PTR>), grid, dim3(WGM * WGN * WGK * 64), 0, \
-                       h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets)
+                       h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets, sym)
     if (!ta && !tb) XRS_GEMM_LAUNCH(false, false);
     else if (!ta && tb) XRS_GEMM_LAUNCH(false, true);
     else if (ta && !tb) XRS_GEMM_LAUNCH(true, false);
@@ -368,7 +384,7 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
 
 template <class PTR>
 static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t Ns, double alpha, size_t lda, bool ta,
-                      size_t Ks, size_t ldb, bool tb) {
+                      size_t Ks, size_t ldb, bool tb, bool sym = false) {
     const int M = int(Ms), N = int(Ns), K = int(Ks);
     // Tile choice (XRS_GEMM_CFG="variant,kmin,target" overrides for tuning experiments):
     //   v1 128x128 (8 waves 2x4)              large problems
@@ -387,7 +403,26 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     auto ntiles = [&](int bm, int bn) { return long(count) * ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     const int bms[10] = {0, 128, 64, 64, 32, 64, 64, 64, 64, 32}, bns[10] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32};
     int var = cfg_var;
-    if (var == 0) {
+    long cfg_target_eff = cfg_target;
+    static const long sym_target = [] {
+        const char* e = std::getenv("XRS_GEMM_SYM_TARGET");
+        return e ? std::atol(e) : 160L;   // measured: 160 -> 1.367 ms/step, 384 -> 1.390, 512 -> 1.398, 256 -> 1.481
+    }();
+    if (sym) cfg_target_eff = sym_target;
+    if (sym) {
+        // symmetric result: square tiles only (32, 64, 128), counted over the lower triangle
+        auto lower = [&](int b) { const long T = (M + b - 1) / b; return long(count) * T * (T + 1) / 2; };
+        auto ntl = [&](int v) { return lower(bms[v]); };
+        var = 4;
+        if (lower(128) >= 1000) var = 1;
+        else if (lower(64) >= 512) var = 2;
+        else if (lower(32) < 512)
+            for (int v : {1, 2, 4}) {
+                const long t = ntl(v);
+                const long sp = std::min<long>((cfg_target_eff + t - 1) / t, std::max<long>(1, K / cfg_kmin));
+                if (t * sp >= cfg_target_eff) { var = v; break; }
+            }
+    } else if (var == 0) {
         // measured on the TT shapes (tools/gemm_tt_bench.py, profiles/r01/gemm_tt_sweep*.txt; the 32x32
         // and 64x32 tiles use a 2-deep ring since the waitcnt fix: 24.6 vs 27.2 us on 256x5120x256):
         //   256 x 5120 x 256 wide/tall: 32x32 24.8 us < 64x32 26.8 < 64x64 28.6 < 128x128 44.5 (alone;
@@ -408,16 +443,17 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
             var = 4;
             for (int v : {1, 2, 3}) {
                 const long t = ntiles(bms[v], bns[v]);
-                const long sp = std::min<long>((cfg_target + t - 1) / t, std::max<long>(1, K / cfg_kmin));
+                const long sp = std::min<long>((cfg_target_eff + t - 1) / t, std::max<long>(1, K / cfg_kmin));
                 if (prefer_inlaunch && sp * bms[v] * bns[v] * 8 > 65536) continue;
-                if (t * sp >= cfg_target) { var = v; break; }
+                if (t * sp >= cfg_target_eff) { var = v; break; }
             }
         }
     }
-    const long tiles = ntiles(bms[var], bns[var]);
+    const long tiles = sym ? long(count) * ((M + bms[var] - 1) / bms[var]) * ((M + bms[var] - 1) / bms[var] + 1) / 2
+                           : ntiles(bms[var], bns[var]);
     int splits = 1;
-    if (tiles < cfg_target) {
-        const long want = (cfg_target + tiles - 1) / tiles;
+    if (tiles < cfg_target_eff) {
+        const long want = (cfg_target_eff + tiles - 1) / tiles;
         const long maxs = std::max<long>(1, K / cfg_kmin);
         splits = int(std::max<long>(1, std::min(want, maxs)));
     }
@@ -440,7 +476,7 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= slab_cap && bms[var] * bns[var] <= 4096;
     int* tickets = (splits > 1 && !two_kernel && small_slab && ntiles(bms[var], bns[var]) <= xrs_handle_s::kTicketCap)
                        ? h->tickets : nullptr;
-#define XRS_TILES(...) launch_tiles<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets)
+#define XRS_TILES(...) launch_tiles<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets, sym ? 1 : 0)
     switch (var) {
         case 1: XRS_TILES(128, 128, 16, 2, 4, 1, 2); break;
         case 2: XRS_TILES(64, 64, 16, 2, 4, 1, 4); break;
@@ -458,7 +494,7 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
         KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
         hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab.d(), MN,
-                           splits, alpha);
+                           splits, alpha, sym ? N : 0);
         check_launch("k_splitk_reduce");
     }
 }
@@ -474,8 +510,20 @@ void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const d
     gemm_impl(h, GemmOne{A, B, C}, 1, Ms, Ns, alpha, lda, ta, Ks, ldb, tb);
 }
 
+void gemm_sym(xrs_handle_t h, double* C, size_t Ns, double alpha, const double* A, size_t lda, bool ta, size_t Ks,
+              const double* B, size_t ldb, bool tb) {
+    if (Ns == 0) return;
+    XRS_REQUIRE(Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
+    if (Ks == 0) {
+        XRS_HIP(hipMemsetAsync(C, 0, Ns * Ns * 8, h->stream));
+        return;
+    }
+    gemm_impl(h, GemmOne{A, B, C}, 1, Ns, Ns, alpha, lda, ta, Ks, ldb, tb, true);
+}
+
 void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t Ns, double alpha, const double* const* A,
-                  size_t lda, bool ta, size_t Ks, const double* const* B, size_t ldb, bool tb) {
+                  size_t lda, bool ta, size_t Ks, const double* const* B, size_t ldb, bool tb, bool sym) {
+    XRS_REQUIRE(!sym || Ms == Ns, "symmetric batch needs square results");
     if (Ms == 0 || Ns == 0 || count <= 0) return;
     XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
     if (Ks == 0) {
@@ -490,7 +538,7 @@ void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t
             P.B[i] = B[b0 + i];
             P.C[i] = C[b0 + i];
         }
-        gemm_impl(h, P, c, Ms, Ns, alpha, lda, ta, Ks, ldb, tb);
+        gemm_impl(h, P, c, Ms, Ns, alpha, lda, ta, Ks, ldb, tb, sym);
     }
 }
 
@@ -523,6 +571,19 @@ extern "C" int xrs_gemm_batched(xrs_handle_t h, size_t count, double* const* C, 
             XRS_REQUIRE(K == 0 || M == 0 || N == 0 || (A[i] && B[i]), "null A/B");
             XRS_REQUIRE(C[i] != A[i] && C[i] != B[i], "C must not alias A or B");
         }
-        xrs::gemm_batched(h, int(count), C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
+        xrs::gemm_batched(h, int(count), C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0, false);
+    });
+}
+
+extern "C" int xrs_gemm_sym(xrs_handle_t h, double* C, size_t N, double alpha, const double* A, size_t lda, int transA,
+                            size_t K, const double* B, size_t ldb, int transB) {
+    return xrs::guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        XRS_REQUIRE(N == 0 || C, "null C");
+        XRS_REQUIRE(K == 0 || N == 0 || (A && B), "null A/B");
+        XRS_REQUIRE(transA ? lda >= N || K == 0 : lda >= K || N == 0, "lda too small");
+        XRS_REQUIRE(transB ? ldb >= K || N == 0 : ldb >= N || K == 0, "ldb too small");
+        XRS_REQUIRE(C != A && C != B, "C must not alias A or B");
+        xrs::gemm_sym(h, C, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
     });
 }

@@ -242,13 +242,13 @@ constexpr double kGramShift = 1e-11;
 void left_gram_step(TT& t, std::vector<DevBuf>& G, double* T, size_t k) {   // G_{k+1} from G_k (G_1 at k = 0)
     xrs_handle_t h = t.h;
     if (k == 0) {
-        gemm(h, G[1].d(), t.r[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
+        gemm_sym(h, G[1].d(), t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
         t.reduce(G[1].d(), t.r[1] * t.r[1]);
         return;
     }
     const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
     gemm(h, T, a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
-    gemm(h, G[k + 1].d(), b, b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);
+    gemm_sym(h, G[k + 1].d(), b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);   // M^T (G M): symmetric
     t.reduce(G[k + 1].d(), b * b);
 }
 
@@ -257,13 +257,13 @@ void right_gram_step(TT& t, std::vector<DevBuf>& H, double* T, size_t k) {   // 
     const size_t last = t.d - 1;
     if (k == last) {
         const size_t cl = t.cols_right(last);
-        gemm(h, H[last].d(), t.r[last], t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
+        gemm_sym(h, H[last].d(), t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
         t.reduce(H[last].d(), t.r[last] * t.r[last]);
         return;
     }
     const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
     gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
-    gemm(h, H[k].d(), a, a, 1.0, t.core[k], cols, false, cols, T, cols, true);         // M_k T^T
+    gemm_sym(h, H[k].d(), a, 1.0, t.core[k], cols, false, cols, T, cols, true);        // M_k T^T: symmetric
     t.reduce(H[k].d(), a * a);
 }
 
@@ -370,6 +370,7 @@ struct GemmJob {
     const double* A;
     const double* B;
     double* C;
+    bool sym = false;   // result known symmetric (M == N): lower tiles only, mirrored
 };
 
 void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
@@ -382,15 +383,17 @@ void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
         for (size_t j = i; j < jobs.size(); ++j) {
             const GemmJob& o = jobs[j];
             if (done[j] || o.M != g.M || o.N != g.N || o.K != g.K || o.lda != g.lda || o.ldb != g.ldb || o.ta != g.ta ||
-                o.tb != g.tb)
+                o.tb != g.tb || o.sym != g.sym)
                 continue;
             done[j] = true;
             A.push_back(o.A);
             B.push_back(o.B);
             C.push_back(o.C);
         }
-        if (C.size() == 1) gemm(h, C[0], g.M, g.N, 1.0, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
-        else gemm_batched(h, int(C.size()), C.data(), g.M, g.N, 1.0, A.data(), g.lda, g.ta, g.K, B.data(), g.ldb, g.tb);
+        if (C.size() == 1 && g.sym) gemm_sym(h, C[0], g.N, 1.0, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
+        else if (C.size() == 1) gemm(h, C[0], g.M, g.N, 1.0, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
+        else gemm_batched(h, int(C.size()), C.data(), g.M, g.N, 1.0, A.data(), g.lda, g.ta, g.K, B.data(), g.ldb, g.tb,
+                          g.sym);
     }
 }
 
@@ -528,7 +531,7 @@ double chain_check(TT& t, const std::vector<double*>& C) {
     std::vector<GemmJob> grams;
     for (size_t k = 1; k < d; ++k) {
         const size_t a = t.r[k], cols = t.cols_right(k);
-        grams.push_back({a, a, cols, cols, cols, false, true, C[k], C[k], Gr[k].d()});
+        grams.push_back({a, a, cols, cols, cols, false, true, C[k], C[k], Gr[k].d(), true});
     }
     gemm_grouped(h, grams);
     if (t.sharded())   // complete the mode sums across ranks
