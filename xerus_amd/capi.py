@@ -351,15 +351,24 @@ class TTDevice:
         return out
 
     def _arrays(self):
+        # ctypes views are cached and reused while r / ptrs are the lists the last call produced (the C
+        # side updates them in place); ~16 us of Python per call otherwise
+        c = getattr(self, "_cache", None)
+        if c is not None and c[3] is self.r and c[4] is self.ptrs:
+            return c[0], c[1], c[2]
         d = self.order
         n = _arr(self.dims)
         r = _arr(self.r)
-        cores = (_DP * d)(*[_DP(p) for p in self.ptrs])
+        cores = (_DP * d)(*self.ptrs)
+        self._cache = (n, r, cores, self.r, self.ptrs)
         return n, r, cores
 
     def _writeback(self, r, cores):
-        self.r = [int(r[i]) for i in range(self.order + 1)]
-        self.ptrs = [int(cores[i] or 0) for i in range(self.order)]
+        self.r = r[:]
+        self.ptrs = [p or 0 for p in cores[:]]
+        c = getattr(self, "_cache", None)
+        if c is not None and c[1] is r and c[2] is cores:
+            self._cache = (c[0], r, cores, self.r, self.ptrs)
 
     def move_core(self, position: int, keep_rank: bool = False):
         n, r, cores = self._arrays()
@@ -374,7 +383,12 @@ class TTDevice:
         if isinstance(max_ranks, (int, np.integer)):
             max_ranks = [int(max_ranks)] * (d - 1)
         n, r, cores = self._arrays()
-        mr = _arr(list(max_ranks) + [1])
+        key = tuple(max_ranks)
+        mc = getattr(self, "_mr_cache", None)
+        if mc is None or mc[0] != key:
+            mc = (key, _arr(list(max_ranks) + [1]))
+            self._mr_cache = mc
+        mr = mc[1]
         st = self.handle.lib.xrs_tt_round(self.handle.h, d, n, r, cores, int(self.canonicalized), self.core_position,
                                           mr, eps)
         self._writeback(r, cores)
@@ -383,12 +397,9 @@ class TTDevice:
 
     def dot(self, other: "TTDevice") -> float:
         out = C.c_double()
-        d = self.order
-        n = _arr(self.dims)
-        xc = (_DP * d)(*[_DP(p) for p in self.ptrs])
-        yc = (_DP * d)(*[_DP(p) for p in other.ptrs])
-        _check("xrs_tt_dot", self.handle.lib.xrs_tt_dot(self.handle.h, C.byref(out), d, n, _arr(self.r), xc,
-                                                      _arr(other.r), yc))
+        n, rx, xc = self._arrays()
+        _, ry, yc = other._arrays()
+        _check("xrs_tt_dot", self.handle.lib.xrs_tt_dot(self.handle.h, C.byref(out), self.order, n, rx, xc, ry, yc))
         return out.value
 
     def frob_norm(self) -> float:
