@@ -54,9 +54,17 @@ def _worker(rank, world, port, backend, out):
         d_sh = sx.dot(sy, comm)
         d_ref = ref.dot(x, y)
         nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
+        # odd order: the two-ended zipper's left end idles in the last step
+        dims7, ranks7 = [5, 6, 4, 7, 5, 6, 4], [5, 9, 11, 9, 8, 4]
+        x7 = ref.TT.random_raw(dims7, ranks7, ref.Rng(41))
+        y7 = ref.TT.random_raw(dims7, ranks7, ref.Rng(43))
+        d7 = xd.ShardedTT.from_full_cores(h, x7.cores, world, rank).dot(
+            xd.ShardedTT.from_full_cores(h, y7.cores, world, rank), comm)
+        n7 = np.sqrt(ref.dot(x7, x7) * ref.dot(y7, y7))
+        dot7_err = abs(d7 - ref.dot(x7, y7)) / n7
         cert = sx.round(12, comm)
         full = sx.gather(dist.all_gather_object)
-        res = {"dot_err": abs(d_sh - d_ref) / (nx * ny), "cert": cert, "ranks": sx.ranks}
+        res = {"dot_err": abs(d_sh - d_ref) / (nx * ny), "dot7_err": dot7_err, "cert": cert, "ranks": sx.ranks}
         if rank == 0:
             xr = x.copy()
             xr.round(12)
@@ -87,6 +95,7 @@ def test_sharded_round_and_dot(world, backend):
     for rank in range(world):
         r = out[rank]
         assert r["dot_err"] <= 1e-12
+        assert r["dot7_err"] <= 1e-12
         assert r["cert"] is True
         assert r["ranks"] == r0["ref_ranks"]
         assert r["cert_sum"] is False and r["untouched"]

@@ -29,6 +29,9 @@ def _tt_diff_norm(ref, a_cores, b_cores):
 
 @pytest.mark.parametrize("dims,ranks", [
     ([4, 5, 3, 4, 2], [3, 6, 5, 2]),
+    ([3, 4, 5, 4, 3, 4, 5], [4, 6, 8, 6, 4, 3]),   # odd order: the two-ended zipper's left end idles once
+    ([6, 5, 7, 4], [5, 9, 4]),                      # smallest two-ended order
+    ([7, 3, 5], [6, 4]),                            # one-ended (d < 4)
     ([20] * 6, [16] * 5),
     ([20] * 10, [128] * 9),   # cfg3 shape
     ([20] * 12, [256] * 11),  # cfg4 shape

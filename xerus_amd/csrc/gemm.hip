@@ -413,8 +413,13 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         // symmetric result: square tiles only (32, 64, 128), counted over the lower triangle
         auto lower = [&](int b) { const long T = (M + b - 1) / b; return long(count) * T * (T + 1) / 2; };
         auto ntl = [&](int v) { return lower(bms[v]); };
+        static const int sym_var = [] {
+            const char* e = std::getenv("XRS_GEMM_SYM_VAR");   // tuning: force 1, 2 or 4
+            return e ? std::atoi(e) : 0;
+        }();
         var = 4;
-        if (lower(128) >= 1000) var = 1;
+        if (sym_var == 1 || sym_var == 2 || sym_var == 4) var = sym_var;
+        else if (lower(128) >= 1000) var = 1;
         else if (lower(64) >= 512) var = 2;
         else if (lower(32) < 512)
             for (int v : {1, 2, 4}) {

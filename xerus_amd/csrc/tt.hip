@@ -239,54 +239,69 @@ constexpr double kGramShift = 1e-11;
 // Gram chains from the current cores (k = 1..d-1, index k):
 //   left  G_k = X_{<k}^T X_{<k}:  G_1 = M_0^T M_0, G_{k+1} = M_k^T (G_k M_k)   (M_k: r_k x n_k r_{k+1})
 //   right H_k = X_{>=k} X_{>=k}^T: H_{d-1} = M M^T, H_k = M_k (I (x) H_{k+1}) M_k^T
-void left_gram_step(TT& t, std::vector<DevBuf>& G, double* T, size_t k) {   // G_{k+1} from G_k (G_1 at k = 0)
+void left_gram_step(TT& t, std::vector<double*>& G, double* T, size_t k, bool do_reduce = true) {   // G_{k+1} from G_k
     xrs_handle_t h = t.h;
     if (k == 0) {
-        gemm_sym(h, G[1].d(), t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
-        t.reduce(G[1].d(), t.r[1] * t.r[1]);
+        gemm_sym(h, G[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
+        if (do_reduce) t.reduce(G[1], t.r[1] * t.r[1]);
         return;
     }
     const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-    gemm(h, T, a, cols, 1.0, G[k].d(), a, false, a, t.core[k], cols, false);
-    gemm_sym(h, G[k + 1].d(), b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);   // M^T (G M): symmetric
-    t.reduce(G[k + 1].d(), b * b);
+    gemm(h, T, a, cols, 1.0, G[k], a, false, a, t.core[k], cols, false);
+    gemm_sym(h, G[k + 1], b, 1.0, t.core[k], b, true, a * t.n[k], T, b, false);   // M^T (G M): symmetric
+    if (do_reduce) t.reduce(G[k + 1], b * b);
 }
 
-void right_gram_step(TT& t, std::vector<DevBuf>& H, double* T, size_t k) {   // H_k from H_{k+1} (H_{d-1} at k = d-1)
+void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool do_reduce = true) {   // H_k from H_{k+1}
     xrs_handle_t h = t.h;
     const size_t last = t.d - 1;
     if (k == last) {
         const size_t cl = t.cols_right(last);
-        gemm_sym(h, H[last].d(), t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
-        t.reduce(H[last].d(), t.r[last] * t.r[last]);
+        gemm_sym(h, H[last], t.r[last], 1.0, t.core[last], cl, false, cl, t.core[last], cl, true);
+        if (do_reduce) t.reduce(H[last], t.r[last] * t.r[last]);
         return;
     }
     const size_t a = t.r[k], b = t.r[k + 1], cols = t.cols_right(k);
-    gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1].d(), b, false);   // M_k(rn x r') H
-    gemm_sym(h, H[k].d(), a, 1.0, t.core[k], cols, false, cols, T, cols, true);        // M_k T^T: symmetric
-    t.reduce(H[k].d(), a * a);
+    gemm(h, T, a * t.n[k], b, 1.0, t.core[k], b, false, b, H[k + 1], b, false);   // M_k(rn x r') H
+    gemm_sym(h, H[k], a, 1.0, t.core[k], cols, false, cols, T, cols, true);        // M_k T^T: symmetric
+    if (do_reduce) t.reduce(H[k], a * a);
 }
 
-// Both chains; unsharded they run concurrently (left on a side stream, right on the main stream) with
-// their launches interleaved step by step, so that neither stream waits for the host to finish
-// enqueueing the other chain. Every buffer they touch is allocated before the fork and outlives the join.
-void gram_chains(TT& t, std::vector<DevBuf>& G, std::vector<DevBuf>& H, bool left = true) {
+// Both chains (G: left Grams, only with `left`; H: right Grams; `store` owns the memory). Unsharded they
+// run concurrently (left on a side stream, right on the main stream) with their launches interleaved
+// step by step, so that neither stream waits for the host to finish enqueueing the other chain. Sharded,
+// step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s} sit side by side in one buffer.
+void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left = true) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
-    G.clear();
-    H.clear();
-    G.resize(d);
-    H.resize(d);
+    G.assign(d, nullptr);
+    H.assign(d, nullptr);
     size_t tmax = 1;
     for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
-    for (size_t k = 1; k < d; ++k) {
-        if (left) G[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
-        H[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
-    }
     DevBuf TL(h, tmax * 8), TR(h, tmax * 8);
-    if (!left || t.sharded()) {   // (the all-reduce hook synchronises: keep sharded chains on one stream)
-        if (left)
-            for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, TL.d(), k);
+    if (t.sharded()) {
+        for (size_t s = 0; s + 1 < d; ++s) {
+            const size_t kl = s + 1, kr = d - 1 - s;
+            const size_t nl = left ? t.r[kl] * t.r[kl] : 0, nr = t.r[kr] * t.r[kr];
+            store.emplace_back(h, (nl + nr) * 8);
+            double* base = store.back().d();
+            if (left) G[kl] = base;
+            H[kr] = base + nl;
+            if (left) left_gram_step(t, G, TL.d(), s, false);
+            right_gram_step(t, H, TR.d(), kr, false);
+            t.reduce(base, nl + nr);
+        }
+        return;
+    }
+    for (size_t k = 1; k < d; ++k) {
+        if (left) {
+            store.emplace_back(h, t.r[k] * t.r[k] * 8);
+            G[k] = store.back().d();
+        }
+        store.emplace_back(h, t.r[k] * t.r[k] * 8);
+        H[k] = store.back().d();
+    }
+    if (!left) {
         for (size_t k = d - 1; k >= 1; --k) right_gram_step(t, H, TR.d(), k);
         return;
     }
@@ -407,9 +422,10 @@ struct ChainPass {
 void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
-    std::vector<DevBuf> G, H, Lf(d), Cs;
+    std::vector<double*> G, H;
+    std::vector<DevBuf> gram_store, Lf(d), Cs;
     XRS_MARK("pass");
-    gram_chains(t, G, H, certify);
+    gram_chains(t, G, H, gram_store, certify);
     XRS_MARK("chains");
     const int per = certify ? 3 : 1;
     const int cnt = int(per * (d - 1));
@@ -424,7 +440,7 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
         const size_t a = t.r[k], de = dinv_elems(int(a));
         dinv[k] = Dv.d() + off;
         Lf[k] = DevBuf(h, a * a * 8);
-        jobs.push_back({H[k].d(), Lf[k].d(), dinv[k], 0.0, int(a)});
+        jobs.push_back({H[k], Lf[k].d(), dinv[k], 0.0, int(a)});
         if (certify) {   // status-only certificates (the 32-block kernel for n > 256 needs a work copy)
             double* w1 = nullptr;
             double* w2 = nullptr;
@@ -434,8 +450,8 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
                 Cs.emplace_back(h, a * a * 8);
                 w2 = Cs.back().d();
             }
-            jobs.push_back({G[k].d(), w1, Dscr.d() + 2 * off, -kGramShift, int(a)});
-            jobs.push_back({H[k].d(), w2, Dscr.d() + 2 * off + de, -kGramShift, int(a)});
+            jobs.push_back({G[k], w1, Dscr.d() + 2 * off, -kGramShift, int(a)});
+            jobs.push_back({H[k], w2, Dscr.d() + 2 * off + de, -kGramShift, int(a)});
         }
         off += de;
     }
@@ -523,21 +539,23 @@ double chain_check(TT& t, const std::vector<double*>& C) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
     XRS_MARK("check");
-    std::vector<DevBuf> Gr(d);
+    std::vector<double*> Gr(d, nullptr);
     DevIdArgs da{};
     DevBuf dev(h, d * 16 * 8 + 64);
     int nchk = 0;
-    for (size_t k = 1; k < d; ++k) Gr[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
+    size_t gtot = 0;
+    for (size_t k = 1; k < d; ++k) gtot += t.r[k] * t.r[k];
+    DevBuf Gall(h, gtot * 8);   // contiguous: one all-reduce for every Gram when sharded
+    for (size_t k = 1, off = 0; k < d; off += t.r[k] * t.r[k], ++k) Gr[k] = Gall.d() + off;
     std::vector<GemmJob> grams;
     for (size_t k = 1; k < d; ++k) {
         const size_t a = t.r[k], cols = t.cols_right(k);
-        grams.push_back({a, a, cols, cols, cols, false, true, C[k], C[k], Gr[k].d(), true});
+        grams.push_back({a, a, cols, cols, cols, false, true, C[k], C[k], Gr[k], true});
     }
     gemm_grouped(h, grams);
-    if (t.sharded())   // complete the mode sums across ranks
-        for (size_t k = 1; k < d; ++k) t.reduce(Gr[k].d(), t.r[k] * t.r[k]);
+    t.reduce(Gall.d(), gtot);   // sharded: complete the mode sums across ranks (no-op otherwise)
     for (size_t k = 1; k < d; ++k) {
-        da.G[nchk] = Gr[k].d();
+        da.G[nchk] = Gr[k];
         da.n[nchk] = int(t.r[k]);
         ++nchk;
     }
@@ -651,35 +669,51 @@ void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, 
 // independent, so the critical path halves and the two streams fill the chip together.
 //   left  E_{k+1} (rx_{k+1} x ry_{k+1}) = sum_i X_k[:,i,:]^T E_k Y_k[:,i,:]      (E_0 = 1)
 //   right F_k     (rx_k x ry_k)         = sum_i X_k[:,i,:] F_{k+1} Y_k[:,i,:]^T  (F_d = 1)
+// Sharded (mode slices): both ends on one stream, the two environments of a step side by side in one
+// buffer and completed by ONE all-reduce; the closing sum needs none (E_m, F_m are already global).
 double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
-                     const double* const* Y) {
+                     const double* const* Y, const TT* shard = nullptr) {
     const size_t m = d / 2;
     size_t emax = 1, tmax = 1;
     for (size_t k = 0; k <= d; ++k) emax = std::max(emax, rx[k] * ry[k]);
     for (size_t k = 0; k < d; ++k) tmax = std::max(tmax, std::max(ry[k] * n[k] * rx[k + 1], rx[k] * n[k] * ry[k + 1]));
-    DevBuf E0(h, emax * 8), E1(h, emax * 8), F0(h, emax * 8), F1(h, emax * 8), TL(h, tmax * 8), TR(h, tmax * 8);
+    // ping-pong pair buffers [E | F]: E at the front, F right behind the E written in the same step
+    DevBuf P0(h, 2 * emax * 8), P1(h, 2 * emax * 8), TL(h, tmax * 8), TR(h, tmax * 8);
     const double ones[2] = {1.0, 1.0};
-    XRS_HIP(hipMemcpyAsync(E0.d(), &ones[0], 8, hipMemcpyHostToDevice, h->stream));
-    XRS_HIP(hipMemcpyAsync(F0.d(), &ones[1], 8, hipMemcpyHostToDevice, h->stream));
-    double *E = E0.d(), *En = E1.d(), *F = F0.d(), *Fn = F1.d();
+    XRS_HIP(hipMemcpyAsync(P0.d(), &ones[0], 8, hipMemcpyHostToDevice, h->stream));
+    XRS_HIP(hipMemcpyAsync(P0.d() + emax, &ones[1], 8, hipMemcpyHostToDevice, h->stream));
+    double *E = P0.d(), *F = P0.d() + emax;
+    double* nextbuf = P1.d();
+    double* curbuf = P0.d();
     {
         StreamFork fork(h);
         const size_t steps = std::max(m, d - m);
         for (size_t s = 0; s < steps; ++s) {   // launches interleaved step by step (see gram_chains)
+            double* En = E;
+            double* Fn = F;
+            size_t ne = 0, nf = 0;
             if (s < m) {
-                fork.side();
+                if (!shard) fork.side();
                 const size_t k = s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+                En = nextbuf;
+                ne = a2 * b2;
                 gemm(h, TL.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);    // E^T X_k: b x (nk a2)
                 gemm(h, En, a2, b2, 1.0, TL.d(), a2, true, b * nk, Y[k], b2, false);       // ((b nk) x a2)^T Y_k
-                std::swap(E, En);
             }
             if (s < d - m) {
-                fork.main();
+                if (!shard) fork.main();
                 const size_t k = d - 1 - s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+                Fn = nextbuf + (shard ? ne : emax);
+                nf = a * b;
                 gemm(h, TR.d(), a * nk, b2, 1.0, X[k], a2, false, a2, F, b2, false);       // X_k F: (a nk) x b2
                 gemm(h, Fn, a, b, 1.0, TR.d(), nk * b2, false, nk * b2, Y[k], nk * b2, true);   // T Y_k^T: a x b
-                std::swap(F, Fn);
             }
+            // one all-reduce for both ends. The left end is idle only in the last step of an odd order
+            // (d - m = m + 1): E then stays in the other buffer, untouched by this step's F.
+            if (shard) shard->reduce(nextbuf, ne + nf);
+            E = En;
+            F = Fn;
+            std::swap(curbuf, nextbuf);
         }
         fork.join();
     }
@@ -693,7 +727,7 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
         emax = std::max(emax, rx[k + 1] * ry[k + 1]);
         tmax = std::max(tmax, ry[k] * n[k] * rx[k + 1]);
     }
-    if (!shard && d >= 4) return dot_two_ended(h, d, n, rx, X, ry, Y);
+    if (d >= 4) return dot_two_ended(h, d, n, rx, X, ry, Y, shard);
     DevBuf E0(h, emax * 8), E1(h, emax * 8), T(h, tmax * 8);
     const double one = 1.0;
     XRS_HIP(hipMemcpyAsync(E0.d(), &one, 8, hipMemcpyHostToDevice, h->stream));
