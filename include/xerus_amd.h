@@ -151,19 +151,22 @@ int xrs_tt_dot(xrs_handle_t handle, double* result, size_t d, const size_t* n,
 
 /** All-reduce (element-wise sum over all ranks) of `count` doubles at the device pointer `buf`, in place.
  *  Called by the sharded TT entry points with the handle's stream synchronised; returns 0 on success.
- *  The Python layer (xerus_amd.dist) binds it to torch.distributed (RCCL over xGMI on MI355X). */
+ *  The Python layer (xerus_amd.dist) binds it to torch.distributed (RCCL over xGMI on MI355X).
+ *  A NULL hook means one rank: the local sums are final and no synchronisation happens. */
 typedef int (*xrs_allreduce_fn)(void* ctx, double* buf, size_t count);
 
 /** Mode-sharded TT round (no reference counterpart: xerus is single-process).
  *  Each rank holds, for every component k, the mode slices of its own subset (n_local[k] of them) as
  *  an (r_k, n_local[k], r_{k+1}) row-major device array. The Gram chains are sums over the mode index,
- *  completed by one all-reduce of an r x r matrix per edge; the per-core transforms are local.
+ *  completed by one all-reduce per chain step (both chains' r x r Grams together) and one for all
+ *  orthogonality Grams: d + 0 all-reduces per pass; the per-core transforms are local.
  *  *certified = 1: rounded in place (right-canonical, core at 0, ranks unchanged: no cut possible);
  *  *certified = 0: certificate failed, cores untouched (gather and use xrs_tt_round). */
 int xrs_tt_round_sharded(xrs_handle_t handle, size_t d, const size_t* n_local, size_t* r, double** cores,
                          const size_t* max_ranks, double eps, xrs_allreduce_fn allreduce, void* ctx, int* certified);
 
-/** <x,y> of two TTs mode-sharded identically (zipper with one r_x x r_y all-reduce per component). */
+/** <x,y> of two TTs mode-sharded identically (two-ended zipper: one all-reduce per step for both
+ *  environments, ceil(d/2) in all for d >= 4; one per component below). */
 int xrs_tt_dot_sharded(xrs_handle_t handle, double* result, size_t d, const size_t* n_local, const size_t* rx,
                        const double* const* X, const size_t* ry, const double* const* Y, xrs_allreduce_fn allreduce,
                        void* ctx);

@@ -47,9 +47,11 @@ struct TT {
 
     // Mode-sharded TT (xrs_tt_*_sharded): n[] are this rank's slice counts and every sum over the
     // mode index is completed by an all-reduce across ranks; null for a whole TT on one device.
+    // shard_mode without a hook: a single rank (the local sums are the global ones, no synchronisation)
+    bool shard_mode = false;
     xrs_allreduce_fn ar = nullptr;
     void* ar_ctx = nullptr;
-    bool sharded() const { return ar != nullptr; }
+    bool sharded() const { return shard_mode; }
     void reduce(double* buf, size_t count) const {
         if (!ar) return;
         XRS_HIP(hipStreamSynchronize(h->stream));
@@ -814,14 +816,15 @@ int xrs_tt_round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** 
 int xrs_tt_round_sharded(xrs_handle_t h, size_t d, const size_t* n_local, size_t* r, double** cores,
                          const size_t* max_ranks, double eps, xrs_allreduce_fn allreduce, void* ctx, int* certified) {
     return guarded([&] {
-        XRS_REQUIRE(h && certified && allreduce, "null argument");
+        XRS_REQUIRE(h && certified, "null argument");
         XRS_REQUIRE(d >= 2 && n_local && r && cores, "null TT description");
         XRS_REQUIRE(r[0] == 1 && r[d] == 1, "boundary ranks must be 1");
         XRS_REQUIRE(eps < 1.0 && eps >= 0.0, "_eps must be smaller than one.");
         for (size_t k = 0; k + 1 < d; ++k)
             XRS_REQUIRE(max_ranks[k] > 0, "Trying to round a TTTensor to rank 0 is not possible.");
         TT t{h, d, n_local, r, cores};
-        t.ar = allreduce;
+        t.shard_mode = true;
+        t.ar = allreduce;   // null: one rank
         t.ar_ctx = ctx;
         *certified = round_chain(t, max_ranks, eps) ? 1 : 0;
     });
@@ -831,10 +834,11 @@ int xrs_tt_dot_sharded(xrs_handle_t h, double* result, size_t d, const size_t* n
                        const double* const* X, const size_t* ry, const double* const* Y, xrs_allreduce_fn allreduce,
                        void* ctx) {
     return guarded([&] {
-        XRS_REQUIRE(h && result && allreduce, "null argument");
+        XRS_REQUIRE(h && result, "null argument");
         XRS_REQUIRE(d >= 1 && n_local && rx && ry && X && Y, "null TT description");
         TT t{h, d, n_local, const_cast<size_t*>(rx), const_cast<double**>(X)};
-        t.ar = allreduce;
+        t.shard_mode = true;
+        t.ar = allreduce;   // null: one rank
         t.ar_ctx = ctx;
         *result = dot(h, d, n_local, rx, X, ry, Y, &t);
     });

@@ -91,7 +91,8 @@ class TorchAllReduce:
 
     @property
     def c_fn(self):
-        return C.cast(self.fn, C.c_void_p)
+        # one rank: no hook at all (the C side then skips the stream synchronisation a hook needs)
+        return None if self.single else C.cast(self.fn, C.c_void_p)
 
 
 class ShardedTT:
