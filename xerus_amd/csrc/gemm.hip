@@ -420,7 +420,7 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         var = 4;
         if (sym_var == 1 || sym_var == 2 || sym_var == 4) var = sym_var;
         else if (lower(128) >= 1000) var = 1;
-        else if (lower(64) >= 512) var = 2;
+        else if (lower(64) >= 512) var = 2;   // (13 Grams of 512^2: 32x32 unsplit 943 us < 64x64 1165 us)
         else if (lower(32) < 512)
             for (int v : {1, 2, 4}) {
                 const long t = ntl(v);

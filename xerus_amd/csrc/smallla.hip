@@ -743,12 +743,12 @@ __global__ void __launch_bounds__(XRS_POTRF_RR_THREADS) k_potrf_rr(double* __res
 // Independent factorisations, one workgroup each (e.g. the Gram matrices of every TT edge).
 __global__ void __launch_bounds__(POT_THREADS) k_potrf32_batched(PotrfBatch b) {
     const int i = blockIdx.x;
-    potrf32_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
+    potrf32_body(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + b.slot[i], nullptr, b.src[i]);
 }
 
 __global__ void __launch_bounds__(XRS_POTRF_RR_THREADS) k_potrf_rr_batched(PotrfBatch b) {
     const int i = blockIdx.x;
-    XRS_POTRF_RR_BODY(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + i, nullptr, b.src[i]);
+    XRS_POTRF_RR_BODY(b.G[i], b.n[i], b.shift[i], b.Dinv[i], b.status + b.slot[i], nullptr, b.src[i]);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1216,13 +1216,12 @@ void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count) {
         d.Dinv[c] = b.Dinv[i];
         d.shift[c] = b.shift[i];
         d.n[c] = b.n[i];
+        d.slot[c] = i;   // statuses land directly in the caller's order
         (rr ? fl_s : fl_l) += double(b.n[i]) * b.n[i] * b.n[i] / 3.0;
         ++c;
     }
-    // statuses: written back in the caller's order through a small device copy
-    DevBuf st(h, size_t(count) * 4 + 64);
-    small.status = st.as<int>();
-    large.status = st.as<int>() + ns;
+    small.status = b.status;
+    large.status = b.status;
     if (ns) {
         KernelTimer timer(h, XRS_KFAM_QR, fl_s, 0.0);
         hipLaunchKernelGGL(k_potrf_rr_batched, dim3(ns), dim3(XRS_POTRF_RR_THREADS), 0, h->stream, small);
@@ -1232,17 +1231,6 @@ void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count) {
         KernelTimer timer(h, XRS_KFAM_QR, fl_l, 0.0);
         hipLaunchKernelGGL(k_potrf32_batched, dim3(nl), dim3(POT_THREADS), 0, h->stream, large);
         check_launch("k_potrf32_batched");
-    }
-    if (nl == 0) {
-        XRS_HIP(hipMemcpyAsync(b.status, st.d(), size_t(count) * 4, hipMemcpyDeviceToDevice, h->stream));
-    } else {
-        // restore the caller's order (small entries first in st)
-        int is = 0, il = 0;
-        for (int i = 0; i < count; ++i) {
-            const bool rr = dinv_ld(b.n[i]) == 16;
-            const int src = rr ? is++ : ns + il++;
-            XRS_HIP(hipMemcpyAsync(b.status + i, st.as<int>() + src, 4, hipMemcpyDeviceToDevice, h->stream));
-        }
     }
 }
 

@@ -21,6 +21,7 @@ struct PotrfBatch {
     double* Dinv[kPotrfBatchMax];
     double shift[kPotrfBatchMax];
     int n[kPotrfBatchMax];
+    int slot[kPotrfBatchMax];   // entry i writes status[slot[i]] (set by potrf_batched; callers leave it)
     int* status;
 };
 void potrf_batched(xrs_handle_t h, const PotrfBatch& b, int count);
