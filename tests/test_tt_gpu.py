@@ -173,6 +173,23 @@ def test_round_bench_shape(handle, ref):
     assert diff <= 1e-10 * nrm
 
 
+@pytest.mark.parametrize("ranks", [[20, 400, 400, 20], [20, 300, 300, 20]])
+def test_round_ranks_above_256(handle, ref, ranks):
+    """Edges with 256 < r <= 512 factor through the 2 x 2-block Cholesky (factor_big): certified path,
+    exact ranks, right-orthonormal cores, same tensor as the input."""
+    rng = ref.Rng(29)
+    x = ref.TT.random_raw([20] * 5, ranks, rng)
+    g = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    g.round(512)
+    assert g.ranks == ranks
+    gc = g.cores()
+    for c in gc[1:]:
+        M = c.reshape(c.shape[0], -1)
+        assert np.abs(M @ M.T - np.eye(M.shape[0])).max() <= 1e-13
+    diff, nrm = _tt_diff_norm(ref, gc, x.cores)
+    assert diff <= 1e-10 * nrm
+
+
 def test_tt_errors(handle, ref):
     rng = ref.Rng(1)
     x = ref.TT.random([3, 3, 3], [2, 2], rng)

@@ -388,6 +388,7 @@ struct GemmJob {
     const double* B;
     double* C;
     bool sym = false;   // result known symmetric (M == N): lower tiles only, mirrored
+    double alpha = 1.0;
 };
 
 void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
@@ -400,18 +401,216 @@ void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
         for (size_t j = i; j < jobs.size(); ++j) {
             const GemmJob& o = jobs[j];
             if (done[j] || o.M != g.M || o.N != g.N || o.K != g.K || o.lda != g.lda || o.ldb != g.ldb || o.ta != g.ta ||
-                o.tb != g.tb || o.sym != g.sym)
+                o.tb != g.tb || o.sym != g.sym || o.alpha != g.alpha)
                 continue;
             done[j] = true;
             A.push_back(o.A);
             B.push_back(o.B);
             C.push_back(o.C);
         }
-        if (C.size() == 1 && g.sym) gemm_sym(h, C[0], g.N, 1.0, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
-        else if (C.size() == 1) gemm(h, C[0], g.M, g.N, 1.0, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
-        else gemm_batched(h, int(C.size()), C.data(), g.M, g.N, 1.0, A.data(), g.lda, g.ta, g.K, B.data(), g.ldb, g.tb,
-                          g.sym);
+        if (C.size() == 1 && g.sym) gemm_sym(h, C[0], g.N, g.alpha, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
+        else if (C.size() == 1) gemm(h, C[0], g.M, g.N, g.alpha, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
+        else gemm_batched(h, int(C.size()), C.data(), g.M, g.N, g.alpha, A.data(), g.lda, g.ta, g.K, B.data(), g.ldb,
+                          g.tb, g.sym);
     }
+}
+
+// ---- Cholesky for 256 < n <= 512 from the n <= 256 kernels (2 x 2 blocks, n1 = 256, n2 = n - 256):
+//   W = A + shift*I (shift = shift_rel tr A), L11 = chol(W11), Z11 = L11^{-1}, L21 = W21 Z11^T,
+//   L22 = chol(W22 - L21 L21^T); factor jobs also get L = [L11 0; L21 L22] and
+//   Z = L^{-1} = [Z11 0; -Z22 L21 Z11, Z22]. Every step is one batched launch over all jobs, so the
+//   latency is two 256-Cholesky + two 256-inverses instead of one 512-column sequential sweep
+//   (k_potrf32_batched + k_trinv_batched<32>: 1.1 ms per cfg5 pass).
+constexpr int kBigMax = 64;
+struct BigArgs {
+    const double* src[kBigMax];
+    double* w11[kBigMax];
+    double* w21[kBigMax];
+    double* w22[kBigMax];
+    double shift[kBigMax];
+    int n[kBigMax];
+};
+
+__global__ void __launch_bounds__(256) k_split_shift(const BigArgs a) {
+    const int j = blockIdx.y, n = a.n[j], n1 = 256, n2 = n - 256;
+    const double* A = a.src[j];
+    __shared__ double red[4];
+    double tr = 0.0;
+    for (int i = threadIdx.x; i < n; i += 256) tr += A[size_t(i) * n + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = tr;
+    __syncthreads();
+    const double shift = a.shift[j] * (red[0] + red[1] + red[2] + red[3]);
+    const size_t total = size_t(n) * n;
+    for (size_t e = size_t(blockIdx.x) * 256 + threadIdx.x; e < total; e += size_t(gridDim.x) * 256) {
+        const int r = int(e / n), c = int(e - size_t(r) * n);
+        const double v = A[e] + (r == c ? shift : 0.0);
+        if (r < n1 && c < n1) a.w11[j][size_t(r) * n1 + c] = v;
+        else if (r >= n1 && c < n1) a.w21[j][size_t(r - n1) * n1 + c] = v;
+        else if (r >= n1 && c >= n1) a.w22[j][size_t(r - n1) * n2 + (c - n1)] = v;
+    }
+}
+
+struct SubArgs {
+    double* y[kBigMax];
+    const double* x[kBigMax];
+    int count[kBigMax];
+};
+
+__global__ void __launch_bounds__(256) k_sub_batched(const SubArgs a) {   // y -= x
+    const int j = blockIdx.y;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < a.count[j]; e += gridDim.x * 256) a.y[j][e] -= a.x[j][e];
+}
+
+struct AssembleArgs {
+    double* out[kBigMax];   // n x n
+    const double* b11[kBigMax];
+    const double* b21[kBigMax];
+    const double* b22[kBigMax];
+    int n[kBigMax];
+};
+
+__global__ void __launch_bounds__(256) k_assemble_lower(const AssembleArgs a) {   // [B11 0; B21 B22]
+    const int j = blockIdx.y, n = a.n[j], n1 = 256, n2 = n - 256;
+    const size_t total = size_t(n) * n;
+    for (size_t e = size_t(blockIdx.x) * 256 + threadIdx.x; e < total; e += size_t(gridDim.x) * 256) {
+        const int r = int(e / n), c = int(e - size_t(r) * n);
+        double v = 0.0;
+        if (r < n1) v = c < n1 ? a.b11[j][size_t(r) * n1 + c] : 0.0;
+        else v = c < n1 ? a.b21[j][size_t(r - n1) * n1 + c] : a.b22[j][size_t(r - n1) * n2 + (c - n1)];
+        a.out[j][e] = v;
+    }
+}
+
+struct BigJob {
+    const double* src;
+    double shift_rel;
+    int n;
+    double* L;   // factor jobs: full L and Z = L^{-1} (n x n); certificates: both null
+    double* Z;
+};
+
+// Enqueues every job; statuses (2 per job: the two diagonal factorisations) go to status[0 .. 2*jobs).
+void factor_big(xrs_handle_t h, const std::vector<BigJob>& jobs, int* status, std::vector<DevBuf>& keep) {
+    const int nj = int(jobs.size());
+    XRS_REQUIRE(nj <= kBigMax, "factor_big: too many jobs");
+    constexpr int n1 = 256;
+    BigArgs ba{};
+    std::vector<double*> w11(nj), w21(nj), w22(nj), d11(nj), d22(nj), z11(nj), pp(nj);
+    auto buf = [&](size_t elems) { keep.emplace_back(h, std::max<size_t>(elems, 1) * 8); return keep.back().d(); };
+    size_t maxn2 = 0;
+    for (int j = 0; j < nj; ++j) {
+        const int n = jobs[j].n, n2 = n - n1;
+        XRS_REQUIRE(n > n1 && n <= 2 * n1, "factor_big: n out of range");
+        w11[j] = buf(size_t(n1) * n1);
+        w21[j] = buf(size_t(n2) * n1);
+        w22[j] = buf(size_t(n2) * n2);
+        d11[j] = buf(dinv_elems(n1));
+        d22[j] = buf(dinv_elems(n2));
+        z11[j] = buf(size_t(n1) * n1);
+        pp[j] = buf(size_t(n2) * n2);
+        ba.src[j] = jobs[j].src;
+        ba.w11[j] = w11[j];
+        ba.w21[j] = w21[j];
+        ba.w22[j] = w22[j];
+        ba.shift[j] = jobs[j].shift_rel;
+        ba.n[j] = n;
+        maxn2 = std::max(maxn2, size_t(n2));
+    }
+    hipLaunchKernelGGL(k_split_shift, dim3(256, nj), dim3(256), 0, h->stream, ba);
+    check_launch("k_split_shift");
+    auto chol = [&](const std::vector<double*>& W, const std::vector<double*>& D, int first_slot, bool upper_half) {
+        for (int b0 = 0; b0 < nj; b0 += kPotrfBatchMax) {
+            PotrfBatch pb{};
+            const int c = std::min(kPotrfBatchMax, nj - b0);
+            for (int i = 0; i < c; ++i) {
+                pb.src[i] = nullptr;
+                pb.G[i] = W[b0 + i];
+                pb.Dinv[i] = D[b0 + i];
+                pb.shift[i] = 0.0;
+                pb.n[i] = upper_half ? n1 : jobs[b0 + i].n - n1;
+            }
+            pb.status = status + first_slot + b0;
+            potrf_batched(h, pb, c);
+        }
+    };
+    auto inverse = [&](const std::vector<double*>& L, const std::vector<double*>& D, const std::vector<double*>& X,
+                       bool upper_half, const std::vector<int>& which) {
+        TrinvBatch tb{};
+        int c = 0;
+        for (int j : which) {
+            tb.L[c] = L[j];
+            tb.Dinv[c] = D[j];
+            tb.X[c] = X[j];
+            tb.n[c] = upper_half ? n1 : jobs[j].n - n1;
+            ++c;
+        }
+        if (c) trinv_batched(h, tb, c);
+    };
+    std::vector<int> all(nj), fac;
+    for (int j = 0; j < nj; ++j) {
+        all[j] = j;
+        if (jobs[j].L) fac.push_back(j);
+    }
+    chol(w11, d11, 0, true);                     // L11 in w11
+    inverse(w11, d11, z11, true, all);           // Z11
+    std::vector<GemmJob> g1, g2;
+    for (int j = 0; j < nj; ++j) {
+        const size_t n2 = size_t(jobs[j].n - n1);
+        g1.push_back({n2, size_t(n1), size_t(n1), size_t(n1), size_t(n1), false, true, w21[j], z11[j], w21[j] == nullptr ? nullptr : buf(n2 * n1)});
+    }
+    // L21 = W21 Z11^T into fresh buffers (GEMM outputs must not alias inputs)
+    std::vector<double*> l21(nj);
+    for (int j = 0; j < nj; ++j) l21[j] = g1[j].C;
+    gemm_grouped(h, g1);
+    for (int j = 0; j < nj; ++j) {
+        const size_t n2 = size_t(jobs[j].n - n1);
+        g2.push_back({n2, n2, size_t(n1), size_t(n1), size_t(n1), false, true, l21[j], l21[j], pp[j], true});
+    }
+    gemm_grouped(h, g2);                         // P = L21 L21^T (symmetric)
+    SubArgs sa{};
+    for (int j = 0; j < nj; ++j) {
+        sa.y[j] = w22[j];
+        sa.x[j] = pp[j];
+        sa.count[j] = (jobs[j].n - n1) * (jobs[j].n - n1);
+    }
+    hipLaunchKernelGGL(k_sub_batched, dim3(64, nj), dim3(256), 0, h->stream, sa);
+    check_launch("k_sub_batched");
+    chol(w22, d22, nj, false);                   // L22 in w22
+    if (fac.empty()) return;
+    std::vector<double*> z22(nj, nullptr), tt(nj, nullptr), z21(nj, nullptr);
+    for (int j : fac) {
+        const size_t n2 = size_t(jobs[j].n - n1);
+        z22[j] = buf(n2 * n2);
+        tt[j] = buf(n2 * n1);
+        z21[j] = buf(n2 * n1);
+    }
+    inverse(w22, d22, z22, false, fac);          // Z22
+    std::vector<GemmJob> g3, g4;
+    for (int j : fac) {
+        const size_t n2 = size_t(jobs[j].n - n1);
+        g3.push_back({n2, size_t(n1), size_t(n1), size_t(n1), size_t(n1), false, false, l21[j], z11[j], tt[j]});
+    }
+    gemm_grouped(h, g3);                         // T = L21 Z11
+    for (int j : fac) {
+        const size_t n2 = size_t(jobs[j].n - n1);
+        GemmJob g{n2, size_t(n1), n2, n2, size_t(n1), false, false, z22[j], tt[j], z21[j]};
+        g.alpha = -1.0;
+        g4.push_back(g);
+    }
+    gemm_grouped(h, g4);                         // Z21 = -Z22 T
+    AssembleArgs al{}, az{};
+    int c = 0;
+    for (int j : fac) {
+        al.out[c] = jobs[j].L; al.b11[c] = w11[j]; al.b21[c] = l21[j]; al.b22[c] = w22[j]; al.n[c] = jobs[j].n;
+        az.out[c] = jobs[j].Z; az.b11[c] = z11[j]; az.b21[c] = z21[j]; az.b22[c] = z22[j]; az.n[c] = jobs[j].n;
+        ++c;
+    }
+    hipLaunchKernelGGL(k_assemble_lower, dim3(256, c), dim3(256), 0, h->stream, al);
+    check_launch("k_assemble_lower");
+    hipLaunchKernelGGL(k_assemble_lower, dim3(256, c), dim3(256), 0, h->stream, az);
+    check_launch("k_assemble_lower");
 }
 
 struct ChainPass {
@@ -429,37 +628,46 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     XRS_MARK("pass");
     gram_chains(t, G, H, gram_store, certify);
     XRS_MARK("chains");
-    const int per = certify ? 3 : 1;
-    const int cnt = int(per * (d - 1));
+    // edges with r <= 256: one batched register-resident launch; larger (<= 512): factor_big (2 x 2
+    // blocks of the same kernels), which also delivers Z = L^{-1}
+    std::vector<DevBuf> Z(d);
+    for (size_t k = 1; k < d; ++k) Z[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
     size_t dsz = 0;
-    for (size_t k = 1; k < d; ++k) dsz += dinv_elems(int(t.r[k]));
-    DevBuf Dv(h, dsz * 8 + 8), Dscr(h, (certify ? 2 * dsz : 1) * 8 + 8), st(h, size_t(cnt) * 4 + 64);
+    for (size_t k = 1; k < d; ++k)
+        if (t.r[k] <= 256) dsz += dinv_elems(int(t.r[k]));
     std::vector<double*> dinv(d, nullptr);
     struct Job { const double* src; double* G; double* Dinv; double shift; int n; };
     std::vector<Job> jobs;
+    std::vector<BigJob> big;
+    DevBuf Dv(h, dsz * 8 + 8), Dscr(h, (certify ? 2 * dsz : 1) * 8 + 8);
     size_t off = 0;
     for (size_t k = 1; k < d; ++k) {
-        const size_t a = t.r[k], de = dinv_elems(int(a));
-        dinv[k] = Dv.d() + off;
+        const size_t a = t.r[k];
         Lf[k] = DevBuf(h, a * a * 8);
-        jobs.push_back({H[k], Lf[k].d(), dinv[k], 0.0, int(a)});
-        if (certify) {   // status-only certificates (the 32-block kernel for n > 256 needs a work copy)
-            double* w1 = nullptr;
-            double* w2 = nullptr;
-            if (a > 256) {
-                Cs.emplace_back(h, a * a * 8);
-                w1 = Cs.back().d();
-                Cs.emplace_back(h, a * a * 8);
-                w2 = Cs.back().d();
+        if (a > 256) {
+            big.push_back({H[k], 0.0, int(a), Lf[k].d(), Z[k].d()});
+            if (certify) {
+                big.push_back({G[k], -kGramShift, int(a), nullptr, nullptr});
+                big.push_back({H[k], -kGramShift, int(a), nullptr, nullptr});
             }
-            jobs.push_back({G[k], w1, Dscr.d() + 2 * off, -kGramShift, int(a)});
-            jobs.push_back({H[k], w2, Dscr.d() + 2 * off + de, -kGramShift, int(a)});
+            continue;
+        }
+        const size_t de = dinv_elems(int(a));
+        dinv[k] = Dv.d() + off;
+        jobs.push_back({H[k], Lf[k].d(), dinv[k], 0.0, int(a)});
+        if (certify) {   // status-only certificates
+            jobs.push_back({G[k], nullptr, Dscr.d() + 2 * off, -kGramShift, int(a)});
+            jobs.push_back({H[k], nullptr, Dscr.d() + 2 * off + de, -kGramShift, int(a)});
         }
         off += de;
     }
-    for (int b0 = 0; b0 < cnt; b0 += kPotrfBatchMax) {
+    const int cnt_small = int(jobs.size());
+    const int cnt = cnt_small + 2 * int(big.size());
+    DevBuf st(h, size_t(cnt) * 4 + 64);
+    if (!big.empty()) factor_big(h, big, st.as<int>() + cnt_small, Cs);
+    for (int b0 = 0; b0 < cnt_small; b0 += kPotrfBatchMax) {
         PotrfBatch pb{};
-        const int c = std::min(kPotrfBatchMax, cnt - b0);
+        const int c = std::min(kPotrfBatchMax, cnt_small - b0);
         for (int i = 0; i < c; ++i) {
             pb.src[i] = jobs[b0 + i].src;
             pb.G[i] = jobs[b0 + i].G;
@@ -480,14 +688,13 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     // concurrent streams do). The left factor is applied as a GEMM with the explicit inverse
     // Z_k = L_k^{-1} (one batched launch); the check below certifies the result either way.
     out.C.assign(d, nullptr);
-    std::vector<DevBuf> W(d), Z(d);
+    std::vector<DevBuf> W(d);
     TrinvBatch tb{};
     int ninv = 0;
     for (size_t k = 0; k < d; ++k) {
         out.C[k] = t.alloc(t.size(k));
         if (k > 0 && k + 1 < d) W[k] = DevBuf(h, t.size(k) * 8);
-        if (k > 0) {
-            Z[k] = DevBuf(h, t.r[k] * t.r[k] * 8);
+        if (k > 0 && t.r[k] <= 256) {   // (r > 256: Z came from factor_big)
             tb.L[ninv] = Lf[k].d();
             tb.Dinv[ninv] = dinv[k];
             tb.X[ninv] = Z[k].d();
@@ -527,9 +734,8 @@ bool chain_status_ok(const ChainPass& p) {
     for (int i = 0; i < p.count; ++i)
         if (p.status[i] != 0) {
             if (dbg)
-                std::fprintf(stderr, "chain_pass: Cholesky %d of edge %d (%s) failed at column %d\n", i, i / per + 1,
-                             i % per == 0 ? "right factor" : (i % per == 1 ? "left certificate" : "right certificate"),
-                             p.status[i]);
+                std::fprintf(stderr, "chain_pass: factorisation %d of %d (%d per edge r <= 256, then 2 per r > 256 "
+                             "job) failed at column %d\n", i, p.count, per, p.status[i]);
             return false;
         }
     return true;
