@@ -134,8 +134,8 @@ def bench_cfg5(h, xe, world, rank, dist, sync, steps, warmup):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--order", type=int, default=10)
     ap.add_argument("--mode", type=int, default=20)
     ap.add_argument("--rank", type=int, default=256)

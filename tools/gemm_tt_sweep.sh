@@ -1,5 +1,12 @@
-cd "$GRAFT_REPO_ROOT"
-timeout -k 10 120 python -u tools/gemm_tt_bench.py > gpurun_out/gtt_default.log 2>&1 && timeout -k 10 180 python -u tools/gemm_tt_bench.py torch > gpurun_out/gtt_torch.log 2>&1 || exit 1
-for c in 1,256,512 2,256,512 3,256,512 4,256,512 5,256,512 7,256,512 2,128,1024 4,128,1024 3,128,1024 2,256,1024; do
-  XRS_GEMM_CFG=$c timeout -k 10 120 python -u tools/gemm_tt_bench.py > gpurun_out/gtt_$c.log 2>&1 || exit 1
+#!/bin/bash
+# TT-shape GEMM tile sweep (tools/gemm_tt_bench.py per XRS_GEMM_CFG variant); each run time-limited,
+# the chain stops at the first failure. Usage: tools/gemm_tt_sweep.sh TAG cfg1 cfg2 ...
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+TAG=$1; shift
+mkdir -p gpurun_out
+timeout -k 10 120 python -u tools/gemm_tt_bench.py > gpurun_out/gtt_${TAG}_default.log 2>&1 || exit 1
+for c in "$@"; do
+  XRS_GEMM_CFG=$c timeout -k 10 120 python -u tools/gemm_tt_bench.py > gpurun_out/gtt_${TAG}_$c.log 2>&1 || exit 1
 done
+cat gpurun_out/gtt_${TAG}_*.log

@@ -73,7 +73,7 @@ double reduce_to_host(xrs_handle_t h, int mode, const double* x, const double* y
     reduce_to_device(h, mode, x, y, n, out);
     double* host = static_cast<double*>(h->host_scratch);
     XRS_HIP(hipMemcpyAsync(host, out, 8, hipMemcpyDeviceToHost, h->stream));
-    XRS_HIP(hipStreamSynchronize(h->stream));
+    host_wait(h);
     return host[0];
 }
 

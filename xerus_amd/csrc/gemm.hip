@@ -351,8 +351,18 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const PTR ptrs, const dou
             col = i - row * size_t(symN);
             if (col > row) continue;
         }
+        // slabs summed in slice order 0..splits-1 (bitwise identical to the in-launch combine); the loads
+        // of 8 slices are issued together ahead of their dependent adds (one HBM round trip per 8 slices)
         double s = 0.0;
-        for (int z = 0; z < splits; ++z) s += slab[size_t(z) * MN + i];
+        int z = 0;
+        for (; z + 8 <= splits; z += 8) {
+            double v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load(&slab[size_t(z + u) * MN + i]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; z < splits; ++z) s += __builtin_nontemporal_load(&slab[size_t(z) * MN + i]);
         C[i] = alpha * s;
         if (symN) C[col * size_t(symN) + row] = alpha * s;
     }
@@ -391,7 +401,7 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     //   v2  64x64  (8 waves 2x4)              mid-size
     //   v3  64x32  (8 waves 2x2, K split 2)   split-K Gram shapes (r x r, K = n r)
     //   v4  32x32  (8 waves 2x2, K split 2)   TT "wide"/"tall" shapes (M or N = r, other = n r)
-    //   v8/v9: v3/v4 with a 4-deep ring (tuning only)
+    //   v8/v9: v3/v4 with a 4-deep ring; v10-v13: K-step 32 / 4-wave / 16-wave variants (tuning only)
     // split-K brings the grid to ~target workgroups while every split keeps >= kmin of K.
     static int cfg_var = 0, cfg_kmin = 256, cfg_target = 512;
     static bool cfg_read = false;
@@ -401,7 +411,8 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     }
     // (batched: the tile counts are over the whole batch)
     auto ntiles = [&](int bm, int bn) { return long(count) * ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    const int bms[10] = {0, 128, 64, 64, 32, 64, 64, 64, 64, 32}, bns[10] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32};
+    const int bms[14] = {0, 128, 64, 64, 32, 64, 64, 64, 64, 32, 32, 32, 32, 64},
+              bns[14] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32, 32, 32, 32, 32};
     int var = cfg_var;
     long cfg_target_eff = cfg_target;
     static const long sym_target = [] {
@@ -462,11 +473,11 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         const long maxs = std::max<long>(1, K / cfg_kmin);
         splits = int(std::max<long>(1, std::min(want, maxs)));
     }
-    const int bk = (var >= 5 && var <= 7) ? 32 : 16;
+    const int bk = ((var >= 5 && var <= 7) || var == 10 || var == 12 || var == 13) ? 32 : 16;
     int kps = (K + splits - 1) / splits;
     kps = (kps + bk - 1) / bk * bk;
     splits = (K + kps - 1) / kps;
-    if (std::is_same<PTR, GemmMany>::value && var >= 5) var = (var == 5 || var == 8) ? 3 : (var == 9 ? 4 : 2);   // tuning-only tiles: single GEMMs
+    if (std::is_same<PTR, GemmMany>::value && var >= 5) var = (var == 5 || var == 8 || var == 13) ? 3 : ((var == 9 || var >= 10) ? 4 : 2);   // tuning-only tiles: single GEMMs
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
     // one-launch split-K when the tile grid fits the stream's ticket array (XRS_GEMM_SPLITK2=1: old
@@ -491,6 +502,10 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         case 7: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 64, 32, 2, 2, 2, 4); break;
         case 8: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 32, 16, 2, 2, 2, 4); break;
         case 9: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 16, 2, 2, 2, 4); break;
+        case 10: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 32, 2, 2, 2, 2); break;
+        case 11: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 16, 2, 2, 1, 2); break;
+        case 12: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 32, 2, 2, 4, 2); break;
+        case 13: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 32, 32, 2, 2, 2, 2); break;
         default: XRS_TILES(32, 32, 16, 2, 2, 2, 2); break;
     }
 #undef XRS_TILES

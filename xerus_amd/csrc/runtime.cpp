@@ -101,6 +101,18 @@ static int sync_debug() {
     return v;
 }
 
+void host_wait(xrs_handle_t h) {
+    static const bool spin = std::getenv("XRS_SYNC_SPIN") != nullptr;
+    if (!spin) {
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        return;
+    }
+    XRS_HIP(hipEventRecord(h->ev_host, h->stream));
+    hipError_t e;
+    while ((e = hipEventQuery(h->ev_host)) == hipErrorNotReady) __builtin_ia32_pause();
+    XRS_HIP(e);
+}
+
 void check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw Error{XRS_EHIP, std::string(what) + ": " + hipGetErrorString(e)};
@@ -207,6 +219,7 @@ int xrs_create(xrs_handle_t* handle, int device) {
         }
         XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
         XRS_HIP(hipEventCreateWithFlags(&h->ev_aux, hipEventDisableTiming));
+        XRS_HIP(hipEventCreateWithFlags(&h->ev_host, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
         const size_t tbytes = size_t(1 + xrs_handle_s::kSides) * xrs_handle_s::kTicketCap * sizeof(int);
@@ -243,6 +256,7 @@ int xrs_destroy(xrs_handle_t h) {
         }
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
         if (h->ev_aux) (void)hipEventDestroy(h->ev_aux);
+        if (h->ev_host) (void)hipEventDestroy(h->ev_host);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
         (void)hipFree(h->ticket_base);

@@ -774,7 +774,7 @@ double chain_check(TT& t, const std::vector<double*>& C) {
     double* hd = static_cast<double*>(h->host_scratch) + 64;
     XRS_HIP(hipMemcpyAsync(hd, dev.d(), size_t(nchk) * kSlices * 8, hipMemcpyDeviceToHost, h->stream));
     XRS_MARK("enq");
-    XRS_HIP(hipStreamSynchronize(h->stream));
+    host_wait(h);
     XRS_MARK("sync");
     double worst = 0.0;
     for (int i = 0; i < nchk * kSlices; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
@@ -887,9 +887,15 @@ double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx
     for (size_t k = 0; k < d; ++k) tmax = std::max(tmax, std::max(ry[k] * n[k] * rx[k + 1], rx[k] * n[k] * ry[k + 1]));
     // ping-pong pair buffers [E | F]: E at the front, F right behind the E written in the same step
     DevBuf P0(h, 2 * emax * 8), P1(h, 2 * emax * 8), TL(h, tmax * 8), TR(h, tmax * 8);
-    const double ones[2] = {1.0, 1.0};
-    XRS_HIP(hipMemcpyAsync(P0.d(), &ones[0], 8, hipMemcpyHostToDevice, h->stream));
-    XRS_HIP(hipMemcpyAsync(P0.d() + emax, &ones[1], 8, hipMemcpyHostToDevice, h->stream));
+    // boundary environments E_0 = F_d = [1]: with rank-1 ends (every TT) the first product of each end is
+    // 1 * X_k = X_k exactly, so that GEMM (and the upload of the 1s) is skipped
+    const bool unit_l = rx[0] == 1 && ry[0] == 1, unit_r = rx[d] == 1 && ry[d] == 1;
+    if (!unit_l || !unit_r) {
+        double* ones = static_cast<double*>(h->host_scratch) + 4096;   // (a slot no other routine uses)
+        ones[0] = ones[1] = 1.0;
+        XRS_HIP(hipMemcpyAsync(P0.d(), &ones[0], 8, hipMemcpyHostToDevice, h->stream));
+        XRS_HIP(hipMemcpyAsync(P0.d() + emax, &ones[1], 8, hipMemcpyHostToDevice, h->stream));
+    }
     double *E = P0.d(), *F = P0.d() + emax;
     double* nextbuf = P1.d();
     double* curbuf = P0.d();
@@ -905,16 +911,24 @@ double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx
                 const size_t k = s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
                 En = nextbuf;
                 ne = a2 * b2;
-                gemm(h, TL.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);    // E^T X_k: b x (nk a2)
-                gemm(h, En, a2, b2, 1.0, TL.d(), a2, true, b * nk, Y[k], b2, false);       // ((b nk) x a2)^T Y_k
+                const double* T = X[k];
+                if (!(s == 0 && unit_l)) {
+                    gemm(h, TL.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);    // E^T X_k: b x (nk a2)
+                    T = TL.d();
+                }
+                gemm(h, En, a2, b2, 1.0, T, a2, true, b * nk, Y[k], b2, false);            // ((b nk) x a2)^T Y_k
             }
             if (s < d - m) {
                 if (!shard) fork.main();
                 const size_t k = d - 1 - s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
                 Fn = nextbuf + (shard ? ne : emax);
                 nf = a * b;
-                gemm(h, TR.d(), a * nk, b2, 1.0, X[k], a2, false, a2, F, b2, false);       // X_k F: (a nk) x b2
-                gemm(h, Fn, a, b, 1.0, TR.d(), nk * b2, false, nk * b2, Y[k], nk * b2, true);   // T Y_k^T: a x b
+                const double* T = X[k];
+                if (!(s == 0 && unit_r)) {
+                    gemm(h, TR.d(), a * nk, b2, 1.0, X[k], a2, false, a2, F, b2, false);       // X_k F: (a nk) x b2
+                    T = TR.d();
+                }
+                gemm(h, Fn, a, b, 1.0, T, nk * b2, false, nk * b2, Y[k], nk * b2, true);       // T Y_k^T: a x b
             }
             // one all-reduce for both ends. The left end is idle only in the last step of an odd order
             // (d - m = m + 1): E then stays in the other buffer, untouched by this step's F.
@@ -952,7 +966,7 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
     }
     double* hs = static_cast<double*>(h->host_scratch);
     XRS_HIP(hipMemcpyAsync(hs, E, 8, hipMemcpyDeviceToHost, h->stream));
-    XRS_HIP(hipStreamSynchronize(h->stream));
+    host_wait(h);
     return hs[0];
 }
 
