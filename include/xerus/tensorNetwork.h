@@ -48,6 +48,9 @@ class TensorNetwork {
 
     TensorNetwork();
     explicit TensorNetwork(Tensor _tensor);
+    /// an empty graph (no nodes, no tensors): structural copies for contraction planning
+    struct Structure {};
+    explicit TensorNetwork(Structure) {}
     TensorNetwork(const TensorNetwork&) = default;
     TensorNetwork(TensorNetwork&&) = default;
     TensorNetwork& operator=(const TensorNetwork&) = default;
@@ -69,9 +72,15 @@ class TensorNetwork {
     void sanitize();   // drop erased nodes, renumber
 };
 
+class TTTensor;
+
 namespace internal {
 /// best greedy contraction order over the reference's five score functions (contractionHeuristic.cpp)
 std::vector<std::pair<size_t, size_t>> greedy_contraction_order(const TensorNetwork& _net, double* _cost = nullptr);
+/// the 2d+4-node network of value_t(x(i&0) * y(i&0)) in the reference's numbering (x: ghost 0, cores
+/// 1..d, ghost d+1; y: the same + d+2); with null TTs the nodes carry no data (order planning only)
+TensorNetwork tt_pair_network(const std::vector<size_t>& _n, const std::vector<size_t>& _rx, const std::vector<size_t>& _ry,
+                              const TTTensor* _x = nullptr, const TTTensor* _y = nullptr);
 }  // namespace internal
 
 }  // namespace xerus

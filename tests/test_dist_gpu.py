@@ -1,8 +1,9 @@
 """Mode-sharded TT round / <x,y> through the C-ABI (xrs_tt_round_sharded, xrs_tt_dot_sharded).
 
 Two ranks share the box's single GPU (gloo all-reduce with host staging); one rank with the nccl
-(= RCCL) backend exercises the device-native all-reduce path. Parity: same ranks as the oracle's round,
-same represented tensor, <x,y> within 1e-12 ||x|| ||y||.
+(= RCCL) backend and ``force_hook`` exercises the device-native all-reduce path (dist.all_reduce on the
+device buffer through __cuda_array_interface__) and must give the null-hook results. Parity: same ranks
+as the oracle's round, same represented tensor, <x,y> within 1e-12 ||x|| ||y||.
 """
 import os
 import socket
@@ -35,7 +36,7 @@ def _rel_diff(ref, a_cores, b_cores):
     return D.frob_norm() / B.frob_norm()
 
 
-def _worker(rank, world, port, backend, out):
+def _worker(rank, world, port, backend, force, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group(backend, rank=rank, world_size=world)
     try:
@@ -45,7 +46,7 @@ def _worker(rank, world, port, backend, out):
 
         torch.cuda.set_device(0)
         h = capi.Handle(0)
-        comm = xd.TorchAllReduce()
+        comm = xd.TorchAllReduce(force_hook=force)
         dims, ranks = [8, 6, 7, 5, 8, 6], [6, 12, 12, 10, 6]
         x = ref.TT.random_raw(dims, ranks, ref.Rng(31))
         y = ref.TT.random_raw(dims, ranks, ref.Rng(37))
@@ -80,17 +81,27 @@ def _worker(rank, world, port, backend, out):
         res["cert_sum"] = ss.round(100, comm)
         after = ss.local.cores()
         res["untouched"] = all(np.array_equal(a, b) for a, b in zip(before, after))
+        res["calls"] = comm.calls
+        res["device_native"] = comm.device_native
+        if force:   # the same work with no hook (one rank): identical results
+            null = xd.TorchAllReduce()
+            assert null.c_fn is None
+            sx0 = xd.ShardedTT.from_full_cores(h, x.cores, world, rank)
+            sy0 = xd.ShardedTT.from_full_cores(h, y.cores, world, rank)
+            res["dot_null_diff"] = abs(sx0.dot(sy0, null) - d_sh) / (nx * ny)
+            sx0.round(12, null)
+            res["round_null_diff"] = max(float(np.abs(a - b).max()) for a, b in zip(sx0.local.cores(), sx.local.cores()))
         out[rank] = res
         h.close()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,backend", [(2, "gloo"), (1, "nccl")])
-def test_sharded_round_and_dot(world, backend):
+@pytest.mark.parametrize("world,backend,force", [(2, "gloo", False), (1, "nccl", True)])
+def test_sharded_round_and_dot(world, backend, force):
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), backend, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), backend, force, out), nprocs=world, join=True)
     r0 = out[0]
     for rank in range(world):
         r = out[rank]
@@ -101,3 +112,8 @@ def test_sharded_round_and_dot(world, backend):
         assert r["cert_sum"] is False and r["untouched"]
     assert r0["diff"] <= 1e-12
     assert r0["orth"] <= 1e-13
+    assert r0["calls"] > 0
+    if force:
+        assert r0["device_native"] is True
+        assert r0["dot_null_diff"] <= 1e-15
+        assert r0["round_null_diff"] <= 1e-13

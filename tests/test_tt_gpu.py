@@ -198,3 +198,22 @@ def test_tt_errors(handle, ref):
         g.round([0, 2])
     with pytest.raises(capi.XrsError):
         g.move_core(5)
+
+
+def test_round_many_edges_above_256(handle, ref):
+    """Order 25, rank 300: 22 edges with 256 < r <= 512 need 66 factor_big jobs in the certified pass,
+    more than one argument table holds (kBigMax = 64): the jobs go out in chunks."""
+    import bench
+    from ttutil import tt_diff_norm
+
+    d, n, r = 25, 20, 300
+    ranks = bench.tt_ranks(d, n, r)[1:-1]
+    assert sum(1 for q in ranks if q > 256) == 22
+    x = ref.TT.random_raw([n] * d, ranks, ref.Rng(53))
+    g = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    g.round(r)
+    y = x.copy()
+    y.round(r)
+    assert g.ranks == y.ranks == ranks
+    diff, nrm = tt_diff_norm(g.cores(), x.cores)
+    assert diff <= 1e-10 * nrm

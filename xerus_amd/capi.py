@@ -396,6 +396,8 @@ class TTDevice:
         self.canonicalized, self.core_position = True, 0
 
     def dot(self, other: "TTDevice") -> float:
+        if self.dims != other.dims:
+            raise ValueError(f"dot of TTs with different dimensions: {self.dims} vs {other.dims}")
         out = C.c_double()
         n, rx, xc = self._arrays()
         _, ry, yc = other._arrays()

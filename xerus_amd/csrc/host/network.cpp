@@ -363,11 +363,8 @@ static void exchange_heuristic(double& _bestCost, Order& _order, TensorNetwork _
 
 // structural copy of the given nodes (no tensors); links leaving the set become external
 static TensorNetwork stripped_subnet(const TensorNetwork& _net, const std::set<size_t>& _ids) {
-    TensorNetwork s;
-    s.nodes.clear();
+    TensorNetwork s{TensorNetwork::Structure{}};
     s.nodes.resize(_net.nodes.size());
-    s.dimensions.clear();
-    s.externalLinks.clear();
     for (size_t id = 0; id < _net.nodes.size(); ++id) {
         if (!_ids.count(id)) {
             s.nodes[id].erased = true;
@@ -403,6 +400,36 @@ Order greedy_contraction_order(const TensorNetwork& _net, double* _cost) {
     exchange_heuristic(best, order, s);
     if (_cost) *_cost = best;
     return order;
+}
+
+// The network value_t(x(i&0) * y(i&0)) is contracted over, in the reference's node numbering: x's TT
+// network (ghost ones({1}) node 0, components 1..d, ghost d+1; ttNetwork.cpp:57-108), then y's appended
+// by add_network_to_network (ids + d + 2, tensorNetwork.cpp:553-595), the d mode links joined by
+// link_traces_and_fix (:598-675). Without TT data the nodes are stripped (planning only).
+TensorNetwork tt_pair_network(const std::vector<size_t>& _n, const std::vector<size_t>& _rx, const std::vector<size_t>& _ry,
+                              const TTTensor* _x, const TTTensor* _y) {
+    const size_t d = _n.size();
+    XERUS_REQUIRE(d >= 1 && _rx.size() == d + 1 && _ry.size() == d + 1, "tt_pair_network: need d dims and d+1 ranks per TT");
+    TensorNetwork net{TensorNetwork::Structure{}};
+    net.nodes.resize(2 * d + 4);
+    auto build = [&](size_t base, size_t other, const std::vector<size_t>& r, const TTTensor* tt) {
+        net.nodes[base].neighbors = {Link(base + 1, 0, 1, false)};
+        for (size_t k = 0; k < d; ++k) {
+            const size_t id = base + 1 + k;
+            net.nodes[id].neighbors = {Link(id - 1, k == 0 ? 0 : 2, r[k], false), Link(other + 1 + k, 1, _n[k], false),
+                                       Link(id + 1, 0, r[k + 1], false)};
+        }
+        net.nodes[base + d + 1].neighbors = {Link(base + d, 2, 1, false)};
+        if (tt) {
+            net.nodes[base].tensorObject.reset(new Tensor(Tensor::ones({1})));
+            net.nodes[base + d + 1].tensorObject.reset(new Tensor(Tensor::ones({1})));
+            for (size_t k = 0; k < d; ++k) net.nodes[base + 1 + k].tensorObject.reset(new Tensor(tt->components[k]));
+        }
+    };
+    build(0, d + 2, _rx, _x);
+    build(d + 2, 0, _ry, _y);
+    net.require_valid_network();
+    return net;
 }
 
 }  // namespace internal

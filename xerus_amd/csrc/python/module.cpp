@@ -260,4 +260,26 @@ PYBIND11_MODULE(xerus, m) {
         .def(py::self / value_t())
         .def("__copy__", [](const TTTensor& _t) { return TTTensor(_t); });
     m.def("dot", [](const TTTensor& _x, const TTTensor& _y) { return dot(_x, _y); });
+
+    // ------------------------------------------------------------------ generic TensorNetwork path of <x,y>
+    // (contraction order of the reference's heuristics on the 2d+4-node network; host-only planning)
+    m.def("tt_dot_contraction_order", [](const std::vector<size_t>& _n, const std::vector<size_t>& _rx, const std::vector<size_t>& _ry) {
+        return internal::greedy_contraction_order(internal::tt_pair_network(_n, _rx, _ry));
+    });
+    // value_t(x(i&0) * y(i&0)) contracted as a generic TensorNetwork (heuristic order, permutation + GEMM per
+    // pair on the GPU) instead of the TT zipper
+    m.def("tt_dot_network", [](const TTTensor& _x, const TTTensor& _y) {
+        XERUS_REQUIRE(_x.dimensions == _y.dimensions, "dot of TTs with different dimensions");
+        const size_t d = _x.degree();
+        std::vector<size_t> rx(d + 1, 1), ry(d + 1, 1);
+        for (size_t k = 0; k < d; ++k) {
+            rx[k + 1] = _x.components[k].dimensions[2];
+            ry[k + 1] = _y.components[k].dimensions[2];
+        }
+        TensorNetwork net = internal::tt_pair_network(_x.dimensions, rx, ry, &_x, &_y);
+        std::set<size_t> all;
+        for (size_t i = 0; i < net.nodes.size(); ++i) all.insert(i);
+        const size_t res = net.contract(all);
+        return (*net.nodes[res].tensorObject)[0];
+    });
 }

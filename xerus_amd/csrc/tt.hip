@@ -135,23 +135,10 @@ void move_core(TT& t, bool canonicalized, size_t core_pos, size_t pos, bool keep
     }
 }
 
-// left-orthogonalise core k into k+1 keeping the rank (round's canonicalisation sweep)
-void orth_right(TT& t, size_t k) {
-    const size_t m = t.rows_left(k), nn = t.r[k + 1];
-    if (m < nn || nn > size_t(kSmallMax)) {  // wide unfolding: rank must drop to m -> reference QC semantics
-        transfer_right(t, k, true);
-        return;
-    }
-    double* Q = t.alloc(m * nn);
-    double* R = t.alloc(nn * nn);
-    orthogonalize(t.h, t.core[k], m, nn, false, Q, R);
-    const size_t ncols = t.cols_right(k + 1);
-    double* nxt = t.alloc(nn * ncols);
-    gemm(t.h, nxt, nn, ncols, 1.0, R, nn, false, nn, t.core[k + 1], ncols, false);
-    t.release(R);
-    t.replace(k, Q);
-    t.replace(k + 1, nxt);
-}
+// left-orthogonalise core k into k+1 (round's canonicalisation sweep, canonicalize_right ->
+// transfer_core(allowRankReduction = true), tensorNetwork.cpp:842-848): QC with the reference's rank rule
+// |R_kk| < 16 eps R_00 (blasLapackWrapper.cpp:268-272); a certified unfolding keeps its rank without pivoting
+void orth_right(TT& t, size_t k) { transfer_right(t, k, true); }
 
 // svd rank cut of calculate_svd (tensor.cpp:1462-1474): max_rank, then first sigma_j <= eps*sigma_0
 size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps) {
@@ -664,7 +651,10 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     const int cnt_small = int(jobs.size());
     const int cnt = cnt_small + 2 * int(big.size());
     DevBuf st(h, size_t(cnt) * 4 + 64);
-    if (!big.empty()) factor_big(h, big, st.as<int>() + cnt_small, Cs);
+    for (size_t b0 = 0; b0 < big.size(); b0 += kBigMax) {   // chunks of the kernels' argument tables
+        const std::vector<BigJob> part(big.begin() + long(b0), big.begin() + long(std::min(big.size(), b0 + kBigMax)));
+        factor_big(h, part, st.as<int>() + cnt_small + 2 * b0, Cs);
+    }
     for (int b0 = 0; b0 < cnt_small; b0 += kPotrfBatchMax) {
         PotrfBatch pb{};
         const int c = std::min(kPotrfBatchMax, cnt_small - b0);
@@ -1056,6 +1046,8 @@ int xrs_tt_dot_sharded(xrs_handle_t h, double* result, size_t d, const size_t* n
     return guarded([&] {
         XRS_REQUIRE(h && result, "null argument");
         XRS_REQUIRE(d >= 1 && n_local && rx && ry && X && Y, "null TT description");
+        check_tt(d, n_local, rx, const_cast<double* const*>(X));
+        check_tt(d, n_local, ry, const_cast<double* const*>(Y));
         TT t{h, d, n_local, const_cast<size_t*>(rx), const_cast<double**>(X)};
         t.shard_mode = true;
         t.ar = allreduce;   // null: one rank

@@ -55,14 +55,17 @@ class _CudaArray:
 class TorchAllReduce:
     """xrs_allreduce_fn backed by torch.distributed (sum, in place on the device buffer).
 
-    nccl (= RCCL on ROCm) reduces the device buffer directly; gloo reduces a host copy."""
+    nccl (= RCCL on ROCm) reduces the device buffer directly; gloo reduces a host copy. At world size 1
+    no hook is handed to the C side (the local sums are the global ones) unless ``force_hook`` is set:
+    then every reduction still goes through the collective (tests of the RCCL branch on one GPU)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, force_hook: bool = False):
         import torch
         import torch.distributed as dist
 
         self.torch, self.dist, self.group = torch, dist, group
-        self.single = not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1
+        initialized = dist.is_available() and dist.is_initialized()
+        self.single = not initialized or (dist.get_world_size(group) == 1 and not force_hook)
         self.device_native = (not self.single) and dist.get_backend(group) == "nccl"
         self.calls = 0
         self.bytes = 0
@@ -129,6 +132,8 @@ class ShardedTT:
 
     def dot(self, other: "ShardedTT", comm: TorchAllReduce) -> float:
         x, y = self.local, other.local
+        if self.dims != other.dims or x.dims != y.dims:
+            raise ValueError(f"dot of sharded TTs with different dimensions: {self.dims} vs {other.dims}")
         d = x.order
         out = C.c_double()
         xc = (capi._DP * d)(*[capi._DP(p) for p in x.ptrs])
