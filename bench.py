@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # gfx950 dense fp64 matrix peak (MI355X spec)
+HBM_PEAK_GBS = 8000.0           # HBM3E spec peak (MI355X_MICROARCH.md; 6.29 TB/s measured for a float4 copy)
 SEED = 0xBAADF00D               # src/xerus/test/test.cpp:105
 
 
@@ -131,6 +132,174 @@ def bench_cfg5(h, xe, world, rank, dist, sync, steps, warmup):
     return out
 
 
+def _timed(fn, reps, sync):
+    """mean wall ms of fn() over reps calls (one warm-up call first), synchronised on both sides."""
+    fn()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    sync()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def _events(h, mask, fn, reps):
+    """HIP-event timing of every kernel of family `mask` launched by fn() (reps calls): per-launch mean."""
+    from xerus_amd import capi  # noqa: F401
+
+    fn()
+    h.synchronize()
+    h.prof_begin(mask)
+    for _ in range(reps):
+        fn()
+    p = h.prof_end()
+    n = max(1, p["launches"])
+    return {"launches": p["launches"] / reps, "us_per_launch": p["ms"] / n * 1e3, "flops_per_launch": p["flops"] / n,
+            "bytes_per_launch": p["bytes"] / n}
+
+
+def bench_cfg2(h):
+    """BASELINE configs[1]: one dense 1024^3 contraction -> one fp64 MFMA GEMM (inputs resident in HBM)."""
+    from xerus_amd import capi
+
+    n = 1024
+    rng = np.random.default_rng(1)
+    A, B = h.array(rng.standard_normal((n, n))), h.array(rng.standard_normal((n, n)))
+    C = h.empty((n, n))
+    ev = _events(h, capi.KFAM_GEMM, lambda: h.gemm(C, n, n, 1.0, A, n, False, n, B, n, False), 20)
+    tf = 2.0 * n ** 3 / (ev["us_per_launch"] * 1e-6) / 1e12
+    return {"workload": "A(i,j) = B(i,k) * C(k,j), 1024^3, fp64 MFMA GEMM", "us": round(ev["us_per_launch"], 2),
+            "tflops": round(tf, 2), "frac_fp64_peak": round(tf / FP64_MFMA_PEAK_TFLOPS, 3),
+            "timing": "HIP events around the launch, mean of 20"}
+
+
+def bench_cfg1(xe):
+    """BASELINE configs[0] through the C++ host API: A(i,j) = B(i,k,l) * C(k,j,l), 64^3 (permute + GEMM)."""
+    rng = np.random.default_rng(2)
+    B = xe.Tensor.from_ndarray(rng.standard_normal((64, 64, 64)))
+    Cc = xe.Tensor.from_ndarray(rng.standard_normal((64, 64, 64)))
+    i, j, k, l = xe.indices(4)
+    A = xe.Tensor()
+
+    def run():
+        A(i, j) << B(i, k, l) * Cc(k, j, l)
+
+    ms = _timed(run, 50, xe.synchronize)
+    return {"workload": "A(i,j) = B(i,k,l) * C(k,j,l), 64^3, indexed expression (host planning + permute + GEMM)",
+            "us_per_eval": round(ms * 1e3, 1), "gflops": round(2 * 64 ** 4 / (ms * 1e-3) / 1e9, 1)}
+
+
+def bench_permute(h):
+    """Permutation kernels at the shapes on the reference's paths, HBM roofline."""
+    from xerus_amd import capi
+
+    shapes = [("cfg1 C 64^3 {0,2,1}", (64, 64, 64), (0, 2, 1)),
+              ("cfg4 zipper (1,1,256,20,256) {0,1,3,4,2}", (1, 1, 256, 20, 256), (0, 1, 3, 4, 2)),
+              ("1024^2 transpose", (1024, 1024), (1, 0)),
+              ("20^6 reversal", (20,) * 6, (5, 4, 3, 2, 1, 0)),
+              ("4096^2 transpose", (4096, 4096), (1, 0))]
+    out = []
+    for name, dims, shuf in shapes:
+        size = int(np.prod(dims))
+        src = h.array(np.arange(size, dtype=np.float64).reshape(dims))
+        dst = h.empty((size,))
+        ev = _events(h, capi.KFAM_PERMUTE, lambda: h.permute(dst, src, dims, shuf), 20)
+        gbs = 16.0 * size / (ev["us_per_launch"] * 1e-6) / 1e9
+        out.append({"shape": name, "mbytes": round(16.0 * size / 1e6, 2), "us": round(ev["us_per_launch"], 2),
+                    "gbs": round(gbs, 1), "frac_hbm_peak": round(gbs / HBM_PEAK_GBS, 3)})
+        src.free()
+        dst.free()
+    return out
+
+
+def bench_cfg3(h, xe):
+    """BASELINE configs[2]: TTTensor order 10, n 20, rank 128 -- round(128) (certified, non-truncating),
+    round(64) (truncating) and (x + y).round(128) (rank 256 -> 128, rank-revealing left sweep)."""
+    from xerus_amd import capi
+
+    d, n, r = 10, 20, 128
+    dims = [n] * d
+    ranks = tt_ranks(d, n, r)
+    xc = random_cores(xe, dims, ranks, SEED + 11)
+    yc = random_cores(xe, dims, ranks, SEED + 12)
+    x = capi.TTDevice.from_cores(h, xc)
+    x.move_core(0)
+    y = capi.TTDevice.from_cores(h, yc)
+    y.move_core(0)
+    out = {"workload": f"TT order-{d} n={n} rank-{r}"}
+
+    def round_case(src, target, reps):
+        ts = []
+        for _ in range(reps + 1):
+            c = src.clone()
+            h.synchronize()
+            t0 = time.perf_counter()
+            c.round(target)
+            h.synchronize()
+            ts.append(time.perf_counter() - t0)
+            res_ranks = c.r
+            c.free()
+        return float(np.mean(ts[1:])) * 1e3, res_ranks
+
+    ms, rr = round_case(x, 128, 10)
+    f = flops_round(dims, ranks)
+    out["round128"] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_out": rr[1:-1]}
+    ms, rr = round_case(x, 64, 10)
+    out["round64"] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_out": rr[1:-1],
+                      "flops_note": "standard two-sweep flops of the input ranks"}
+    # x + y: block-diagonal cores (TTNetwork::operator+=, ttNetwork.cpp:797-847), not canonical
+    xs, ys = x.cores(), y.cores()
+    sc = []
+    for k in range(d):
+        X, Y = xs[k], ys[k]
+        if k == 0:
+            sc.append(np.concatenate([X, Y], axis=2))
+        elif k == d - 1:
+            sc.append(np.concatenate([X, Y], axis=0))
+        else:
+            Z = np.zeros((X.shape[0] + Y.shape[0], n, X.shape[2] + Y.shape[2]))
+            Z[:X.shape[0], :, :X.shape[2]] = X
+            Z[X.shape[0]:, :, X.shape[2]:] = Y
+            sc.append(Z)
+    s = capi.TTDevice.from_cores(h, sc)
+    sr = [1] + [c.shape[2] for c in sc]
+    ms, rr = round_case(s, 128, 5)
+    f = flops_round(dims, sr)
+    out["sum_round128"] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_in": sr[1:-1],
+                           "ranks_out": rr[1:-1]}
+    for t in (x, y, s):
+        t.free()
+    return out
+
+
+def bench_cfg4(h, xe):
+    """BASELINE configs[3]: <x,x> of a TTTensor order 12, n 20, rank 256 (zipper), fp64 MFMA roofline."""
+    from xerus_amd import capi
+
+    d, n, r = 12, 20, 256
+    dims = [n] * d
+    ranks = tt_ranks(d, n, r)
+    x = capi.TTDevice.from_cores(h, random_cores(xe, dims, ranks, SEED + 13))
+    f = flops_dot(dims, ranks, ranks)
+    ms = _timed(lambda: x.dot(x), 20, h.synchronize)
+    tf = f / (ms * 1e-3) / 1e12
+    x.free()
+    return {"workload": f"<x,x> TT order-{d} n={n} rank-{r}", "ms": round(ms, 4), "gflop": round(f / 1e9, 3),
+            "tflops": round(tf, 2), "frac_fp64_peak": round(tf / FP64_MFMA_PEAK_TFLOPS, 3)}
+
+
+def bench_svd(h):
+    """The dense SVD (xrs_svd, blasWrapper::svd / dgesdd semantics) at the TT edge sizes."""
+    rng = np.random.default_rng(3)
+    out = {}
+    for m in (128, 256, 512):
+        A = h.array(rng.standard_normal((m, m)))
+        ms = _timed(lambda: h.svd(A), 3, h.synchronize)
+        out[str(m)] = {"ms": round(ms, 3)}
+        A.free()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -142,6 +311,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-steps", type=int, default=8)
     ap.add_argument("--no-cfg5", action="store_true", help="skip the sharded order-16 rank-512 round")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the per-config lines (cfg1-cfg4, permutation roofline, SVD); they run at N=1 only")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -237,6 +408,15 @@ def main():
         except Exception as e:   # reported, never fatal for the headline line
             cfg5 = {"error": f"{type(e).__name__}: {e}"}
 
+    extras = {}
+    if world == 1 and not args.no_extras:
+        for key, fn in [("cfg1", lambda: bench_cfg1(xe)), ("cfg2", lambda: bench_cfg2(h)), ("cfg3", lambda: bench_cfg3(h, xe)),
+                        ("cfg4", lambda: bench_cfg4(h, xe)), ("permute", lambda: bench_permute(h)), ("svd", lambda: bench_svd(h))]:
+            try:
+                extras[key] = fn()
+            except Exception as e:   # reported, never fatal for the headline line
+                extras[key] = {"error": f"{type(e).__name__}: {e}"}
+
     if rank == 0:
         launches = max(1, prof["launches"])
         gemm_tflops = prof["flops"] / (prof["ms"] * 1e-3) / 1e12 if prof["ms"] > 0 else 0.0
@@ -314,6 +494,7 @@ def main():
             "cpu_baseline": cpu,
             "cfg5": cfg5,
         }
+        out.update(extras)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

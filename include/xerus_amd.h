@@ -143,6 +143,14 @@ int xrs_tt_move_core(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, 
  *  sigma_j <= eps*sigma_0 (tensor.cpp:1463-1474). On return the core is at position 0. */
 int xrs_tt_round(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
                  int canonicalized, size_t core_position, const size_t* max_ranks, double eps);
+/** Which algorithm the handle's last xrs_tt_round used: XRS_ROUND_CHAIN (certified, no cut possible:
+ *  Gram chains + batched factorisations), XRS_ROUND_TRUNCATE (certified truncation: left chain pass +
+ *  device-resident right-to-left SVD sweep), XRS_ROUND_REFERENCE (the reference's sequential
+ *  QC + round_edge sweeps); 0 before the first round. Diagnostics for tests and benchmarks. */
+#define XRS_ROUND_CHAIN 1
+#define XRS_ROUND_TRUNCATE 2
+#define XRS_ROUND_REFERENCE 3
+int xrs_tt_last_round_path(xrs_handle_t handle);
 /** <x,y> of two TTs with equal mode sizes (value_t(x(i&0)*y(i&0)), ttNetwork.cpp:782-789 path,
  *  SURVEY §3.4) as a left-to-right zipper without permutations. *result on host. Synchronises. */
 int xrs_tt_dot(xrs_handle_t handle, double* result, size_t d, const size_t* n,

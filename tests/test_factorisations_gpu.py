@@ -72,7 +72,8 @@ def test_qr_rq(handle, m, n):
     assert np.linalg.norm(Q2h @ Q2h.T - np.eye(k)) <= TOL * k
 
 
-@pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (64, 64), (128, 128), (30, 200), (200, 30), (1, 5), (5, 1)])
+@pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (64, 64), (128, 128), (30, 200), (200, 30), (1, 5), (5, 1),
+                                 (256, 256), (512, 512), (300, 512), (512, 300), (100, 100), (90, 64)])
 def test_svd(handle, ref, m, n):
     A = np.random.default_rng(m * 5 + n).standard_normal((m, n))
     U, S, Vt = handle.svd(handle.array(A))
@@ -84,6 +85,10 @@ def test_svd(handle, ref, m, n):
     assert _rel((Uh * Sh[None, :]) @ Vh, A) <= TOL
     assert np.linalg.norm(Uh.T @ Uh - np.eye(k)) <= TOL * k
     assert np.linalg.norm(Vh @ Vh.T - np.eye(k)) <= TOL * k
+    # LAPACK-level accuracy (dgesdd measured 1e-15 .. 3e-15 here): the reference's 1e-14 TT tests need it
+    assert _rel((Uh * Sh[None, :]) @ Vh, A) <= 1e-14
+    assert np.abs(Uh.T @ Uh - np.eye(k)).max() <= 1e-14
+    assert np.abs(Vh @ Vh.T - np.eye(k)).max() <= 1e-14
 
 
 def test_svd_rank_deficient(handle, ref):

@@ -113,9 +113,39 @@ def test_round_truncating(handle, ref, dims, ranks, target):
     y.round(target)
     g.round(target)
     assert g.ranks == y.ranks
+    if min(dims) >= 6:   # generic inputs take the certified device-resident truncation
+        assert handle.last_round_path() == "truncate"
     e_ref, nrm = _tt_diff_norm(ref, y.cores, x.cores)
     e_gpu, _ = _tt_diff_norm(ref, g.cores(), x.cores)
     assert abs(e_gpu - e_ref) <= 1e-6 * nrm
+    gc = g.cores()
+    for c in gc[1:]:   # right-canonical result
+        M = c.reshape(c.shape[0], -1)
+        assert np.abs(M @ M.T - np.eye(M.shape[0])).max() <= 1e-12
+
+
+@pytest.mark.parametrize("dims,ranks,target", [([20] * 10, [128] * 9, 128), ([20] * 8, [64] * 7, 40),
+                                               ([6, 5, 7, 4, 6], [6, 12, 12, 6], 10)])
+def test_round_sum_truncating(handle, ref, dims, ranks, target):
+    """(x + y).round(r): doubled ranks with structural excess at both ends (r_1 = 2 n_0 > n_0): the
+    reference's QC drops the left end exactly, the right end goes through the tall-edge SVD; same ranks
+    and truncation error as the oracle's round of the same sum."""
+    from ttutil import tt_diff_norm
+
+    rng = ref.Rng(61)
+    x = ref.TT.random(dims, ranks, rng)
+    y = ref.TT.random(dims, ranks, rng)
+    s = ref.tt_add(x, y)
+    g = capi.TTDevice.from_cores(handle, [c.copy() for c in s.cores])
+    g.round(target)
+    path = handle.last_round_path()
+    o = s.copy()
+    o.round(target)
+    assert g.ranks == o.ranks
+    e_gpu, nrm = tt_diff_norm(g.cores(), s.cores)
+    e_ref, _ = tt_diff_norm(o.cores, s.cores)
+    assert abs(e_gpu - e_ref) <= 1e-6 * nrm, (e_gpu / nrm, e_ref / nrm, path)
+    assert path == "truncate"
 
 
 def test_round_sum_recovers_ranks(handle, ref):

@@ -59,12 +59,14 @@ SIGNATURES = {
                                        C.c_double, _DP, _DP, C.POINTER(C.c_int)]),
     "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                      C.POINTER(_SZ), C.POINTER(_DP), _DP, _DP]),
+    "xrs_tt_last_round_path": (C.c_int, [_DP]),
     "xrs_prof_begin": (C.c_int, [_DP, C.c_uint32]),
     "xrs_prof_end": (C.c_int, [_DP, C.POINTER(_SZ), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                C.POINTER(C.c_double)]),
 }
 
 KFAM_GEMM, KFAM_PERMUTE, KFAM_QR, KFAM_SVD, KFAM_ELEMWISE = 1, 2, 4, 8, 16
+ROUND_PATHS = {0: None, 1: "chain", 2: "truncate", 3: "reference"}
 
 _lib = None
 
@@ -255,6 +257,10 @@ class Handle:
         _check("xrs_svd", self.lib.xrs_svd(self.h, _DP(U.ptr), _DP(S.ptr), _DP(Vt.ptr), _DP(A.ptr), m, n))
         return U, S, Vt
 
+    def last_round_path(self) -> str | None:
+        """"chain" / "truncate" / "reference": the algorithm of this handle's last TT round."""
+        return ROUND_PATHS[self.lib.xrs_tt_last_round_path(self.h)]
+
     # ---- profiling
     def prof_begin(self, mask: int):
         _check("xrs_prof_begin", self.lib.xrs_prof_begin(self.h, mask))
@@ -332,6 +338,16 @@ class TTDevice:
             _check("xrs_upload", handle.lib.xrs_upload(handle.h, _DP(p), c.ctypes.data_as(_DP), c.size))
             ptrs.append(p)
         return cls(handle, dims, ranks, ptrs, canonicalized, core_position)
+
+    def clone(self) -> "TTDevice":
+        """Device-side copy of every core (stream-ordered, no host round trip)."""
+        ptrs = []
+        for k, p in enumerate(self.ptrs):
+            size = self.r[k] * self.dims[k] * self.r[k + 1]
+            q = self.handle.malloc(max(8, size * 8))
+            _check("xrs_copy", self.handle.lib.xrs_copy(self.handle.h, _DP(q), _DP(p), size))
+            ptrs.append(q)
+        return TTDevice(self.handle, self.dims, self.r, ptrs, self.canonicalized, self.core_position)
 
     @property
     def order(self):

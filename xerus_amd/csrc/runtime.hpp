@@ -105,6 +105,8 @@ struct xrs_handle_s {
     int* ticket_base = nullptr;
     int* tickets = nullptr;
     int* side_tickets[kSides] = {};
+    // algorithm of the last TT round (XRS_ROUND_*)
+    int last_round_path = 0;
     // profiler
     uint32_t prof_mask = 0;
     std::vector<xrs::ProfRecord> prof;

@@ -1118,17 +1118,21 @@ __global__ void __launch_bounds__(1024) k_jacobi(double* __restrict__ W, int p, 
                     const double t_ = copysign(1.0, zeta) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
                     const double cs = 1.0 / sqrt(1.0 + t_ * t_);
                     const double sn = cs * t_;
+                    // Rutishauser's form x' = x - s (y + tau x), y' = y + s (x - tau y), tau = s / (1 + c):
+                    // a nearly-identity rotation perturbs the rows by O(u s) instead of O(u), so the
+                    // accumulated J stays orthogonal to working precision over thousands of rotations
+                    const double tau = sn / (1.0 + cs);
                     for (int k = lane; k < q; k += 64) {
                         const double x = wi[k], y = wj[k];
-                        wi[k] = cs * x - sn * y;
-                        wj[k] = sn * x + cs * y;
+                        wi[k] = x - sn * (y + tau * x);
+                        wj[k] = y + sn * (x - tau * y);
                     }
                     double* ji = J + size_t(i) * p;
                     double* jj = J + size_t(j) * p;
                     for (int k = lane; k < p; k += 64) {
                         const double x = ji[k], y = jj[k];
-                        ji[k] = cs * x - sn * y;
-                        jj[k] = sn * x + cs * y;
+                        ji[k] = x - sn * (y + tau * x);
+                        jj[k] = y + sn * (x - tau * y);
                     }
                     if (lane == 0) rotated = 1;
                 }

@@ -48,6 +48,14 @@ size_t qrcp(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, doub
 // One-sided Jacobi SVD of the rows of W (p x q, p <= q): U (p x p), S (p), Vt (p x q), S descending.
 void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, double* S, double* Vt);
 
+// Right singular vectors of W (p x q, p <= min(q, 512); W[i][k] at W[i*ldw + k], or W[k*ldw + i] with
+// trans) by one-sided Jacobi on its rows (svd.hip): S (p) descending, Vt (p x q, row stride ldvt)
+// orthonormal rows, W = U S Vt with U S = W Vt^T. *status_dev = sweeps used, -1 if not converged in
+// max_sweeps. W stays in LDS when p (q + 1) <= 18432 doubles. Enqueued only.
+void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
+               int* status_dev, int max_sweeps = 40);
+bool jacobi_vt_fits_lds(int p, int q);
+
 struct OrthResult {
     bool certified;   // sigma_min(A) >= cert_ratio * ||A||_F proven (Cholesky of the shifted Gram succeeded)
     double cert_ratio;

@@ -24,41 +24,12 @@
 #include <string>
 #include <vector>
 
-#include "smallla.hpp"
+#include "tt_common.hpp"
 
 namespace xrs {
 
-namespace {
+namespace ttd {
 
-struct TT {
-    xrs_handle_t h;
-    size_t d;
-    const size_t* n;
-    size_t* r;      // d + 1 ranks, r[0] = r[d] = 1
-    double** core;
-
-    size_t rows_left(size_t k) const { return r[k] * n[k]; }      // (r_k n_k) x r_{k+1}
-    size_t cols_right(size_t k) const { return n[k] * r[k + 1]; }  // r_k x (n_k r_{k+1})
-    size_t size(size_t k) const { return r[k] * n[k] * r[k + 1]; }
-
-    double* alloc(size_t elems) { return static_cast<double*>(h->pool->alloc(std::max<size_t>(elems, 1) * 8)); }
-    void release(double* p) { if (p) h->pool->release(p); }
-    void replace(size_t k, double* p) { release(core[k]); core[k] = p; }
-
-    // Mode-sharded TT (xrs_tt_*_sharded): n[] are this rank's slice counts and every sum over the
-    // mode index is completed by an all-reduce across ranks; null for a whole TT on one device.
-    // shard_mode without a hook: a single rank (the local sums are the global ones, no synchronisation)
-    bool shard_mode = false;
-    xrs_allreduce_fn ar = nullptr;
-    void* ar_ctx = nullptr;
-    bool sharded() const { return shard_mode; }
-    void reduce(double* buf, size_t count) const {
-        if (!ar) return;
-        XRS_HIP(hipStreamSynchronize(h->stream));
-        const int rc = ar(ar_ctx, buf, count);
-        XRS_REQUIRE(rc == 0, "all-reduce callback failed");
-    }
-};
 
 // reduce_to_maximal_ranks (ttNetwork.cpp:370-402)
 std::vector<size_t> maximal_ranks(const TT& t) {
@@ -223,12 +194,11 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
 //   then sigma_min(U)/sigma_max(U) >= c_X c_L > eps (>= 16 eps needed for the QC rule too, since
 //   |R_kk| >= sigma_min for any triangular factor).
 // Any failed obligation falls back to the reference's two-sweep algorithm, from the failing edge on.
-constexpr double kGramShift = 1e-11;
 
 // Gram chains from the current cores (k = 1..d-1, index k):
 //   left  G_k = X_{<k}^T X_{<k}:  G_1 = M_0^T M_0, G_{k+1} = M_k^T (G_k M_k)   (M_k: r_k x n_k r_{k+1})
 //   right H_k = X_{>=k} X_{>=k}^T: H_{d-1} = M M^T, H_k = M_k (I (x) H_{k+1}) M_k^T
-void left_gram_step(TT& t, std::vector<double*>& G, double* T, size_t k, bool do_reduce = true) {   // G_{k+1} from G_k
+void left_gram_step(TT& t, std::vector<double*>& G, double* T, size_t k, bool do_reduce) {   // G_{k+1} from G_k
     xrs_handle_t h = t.h;
     if (k == 0) {
         gemm_sym(h, G[1], t.r[1], 1.0, t.core[0], t.r[1], true, t.rows_left(0), t.core[0], t.r[1], false);
@@ -241,7 +211,7 @@ void left_gram_step(TT& t, std::vector<double*>& G, double* T, size_t k, bool do
     if (do_reduce) t.reduce(G[k + 1], b * b);
 }
 
-void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool do_reduce = true) {   // H_k from H_{k+1}
+void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool do_reduce) {   // H_k from H_{k+1}
     xrs_handle_t h = t.h;
     const size_t last = t.d - 1;
     if (k == last) {
@@ -260,7 +230,7 @@ void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool d
 // run concurrently (left on a side stream, right on the main stream) with their launches interleaved
 // step by step, so that neither stream waits for the host to finish enqueueing the other chain. Sharded,
 // step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s} sit side by side in one buffer.
-void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left = true) {
+void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
     G.assign(d, nullptr);
@@ -325,11 +295,6 @@ HostMarks::~HostMarks() {
 }
 #define XRS_MARK(what) do { if (g_marks) g_marks->mark(what); } while (0)
 
-struct DevIdArgs {
-    const double* G[64];
-    int n[64];
-    double* out;
-};
 
 // max |G_i - I| of a batch of square matrices, one workgroup each
 __global__ void __launch_bounds__(256) k_dev_identity_many(const DevIdArgs args) {
@@ -357,7 +322,6 @@ __global__ void __launch_bounds__(256) k_dev_identity_many(const DevIdArgs args)
 
 void rl_sweep(TT& t, const size_t* max_ranks, double eps, double cX, size_t from);
 
-constexpr double kOrthTol = 1e-13;   // max |C_k C_k^T - I| accepted for the right-canonical cores
 
 // One chain orthogonalisation pass over the current cores: the right Gram chain H_k (and, with
 // `certify`, the left chain G_k), ONE batched launch of all Cholesky factorisations -- H_k = L_k L_k^T
@@ -368,15 +332,6 @@ constexpr double kOrthTol = 1e-13;   // max |C_k C_k^T - I| accepted for the rig
 // behind the transforms and judged by chain_check (a failed factorisation only makes C garbage, which
 // is then discarded).
 // Independent GEMMs; the ones of identical shape go out as one batched launch.
-struct GemmJob {
-    size_t M, N, K, lda, ldb;
-    bool ta, tb;
-    const double* A;
-    const double* B;
-    double* C;
-    bool sym = false;   // result known symmetric (M == N): lower tiles only, mirrored
-    double alpha = 1.0;
-};
 
 void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
     std::vector<bool> done(jobs.size(), false);
@@ -408,7 +363,6 @@ void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
 //   Z = L^{-1} = [Z11 0; -Z22 L21 Z11, Z22]. Every step is one batched launch over all jobs, so the
 //   latency is two 256-Cholesky + two 256-inverses instead of one 512-column sequential sweep
 //   (k_potrf32_batched + k_trinv_batched<32>: 1.1 ms per cfg5 pass).
-constexpr int kBigMax = 64;
 struct BigArgs {
     const double* src[kBigMax];
     double* w11[kBigMax];
@@ -470,13 +424,6 @@ __global__ void __launch_bounds__(256) k_assemble_lower(const AssembleArgs a) { 
     }
 }
 
-struct BigJob {
-    const double* src;
-    double shift_rel;
-    int n;
-    double* L;   // factor jobs: full L and Z = L^{-1} (n x n); certificates: both null
-    double* Z;
-};
 
 // Enqueues every job; statuses (2 per job: the two diagonal factorisations) go to status[0 .. 2*jobs).
 void factor_big(xrs_handle_t h, const std::vector<BigJob>& jobs, int* status, std::vector<DevBuf>& keep) {
@@ -852,7 +799,11 @@ void rl_sweep(TT& t, const size_t* max_ranks, double eps, double cX, size_t from
 
 void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
-    if (round_chain(t, max_ranks, eps)) return;
+    t.h->last_round_path = XRS_ROUND_CHAIN;
+    if (round_chain(t, max_ranks, eps)) return;      // certified, nothing to cut
+    t.h->last_round_path = XRS_ROUND_TRUNCATE;
+    if (round_truncate(t, max_ranks, eps)) return;   // certified, cuts by maxRank only (tt_trunc.hip)
+    t.h->last_round_path = XRS_ROUND_REFERENCE;
     // canonicalize_right (ttNetwork.cpp:638-640, 654)
     const size_t start = canonicalized ? core_pos : 0;
     for (size_t k = start; k + 1 < d; ++k) orth_right(t, k);
@@ -970,7 +921,9 @@ void check_tt(size_t d, const size_t* n, const size_t* r, double* const* cores) 
     }
 }
 
-}  // namespace
+}  // namespace ttd
+
+using namespace ttd;
 
 namespace tt {
 void move_core(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
@@ -1055,6 +1008,8 @@ int xrs_tt_dot_sharded(xrs_handle_t h, double* result, size_t d, const size_t* n
         *result = dot(h, d, n_local, rx, X, ry, Y, &t);
     });
 }
+
+int xrs_tt_last_round_path(xrs_handle_t h) { return h ? h->last_round_path : -1; }
 
 int xrs_tt_dot(xrs_handle_t h, double* result, size_t d, const size_t* n, const size_t* rx, const double* const* X,
                const size_t* ry, const double* const* Y) {

@@ -1,0 +1,96 @@
+// Internal interface of the TT drivers (tt.hip: move_core, certified chain round, <x,y>; tt_trunc.hip:
+// the certified truncating round). Not part of the C-ABI.
+#pragma once
+#include <vector>
+
+#include "smallla.hpp"
+
+namespace xrs {
+namespace ttd {
+
+struct TT {
+    xrs_handle_t h;
+    size_t d;
+    const size_t* n;
+    size_t* r;      // d + 1 ranks, r[0] = r[d] = 1
+    double** core;
+
+    size_t rows_left(size_t k) const { return r[k] * n[k]; }      // (r_k n_k) x r_{k+1}
+    size_t cols_right(size_t k) const { return n[k] * r[k + 1]; }  // r_k x (n_k r_{k+1})
+    size_t size(size_t k) const { return r[k] * n[k] * r[k + 1]; }
+
+    double* alloc(size_t elems) { return static_cast<double*>(h->pool->alloc(std::max<size_t>(elems, 1) * 8)); }
+    void release(double* p) { if (p) h->pool->release(p); }
+    void replace(size_t k, double* p) { release(core[k]); core[k] = p; }
+
+    // Mode-sharded TT (xrs_tt_*_sharded): n[] are this rank's slice counts and every sum over the
+    // mode index is completed by an all-reduce across ranks; null for a whole TT on one device.
+    // shard_mode without a hook: a single rank (the local sums are the global ones, no synchronisation)
+    bool shard_mode = false;
+    xrs_allreduce_fn ar = nullptr;
+    void* ar_ctx = nullptr;
+    bool sharded() const { return shard_mode; }
+    void reduce(double* buf, size_t count) const {
+        if (!ar) return;
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        const int rc = ar(ar_ctx, buf, count);
+        XRS_REQUIRE(rc == 0, "all-reduce callback failed");
+    }
+};
+
+// reduce_to_maximal_ranks (ttNetwork.cpp:370-402) of the internal ranks; true if any rank exceeds it
+std::vector<size_t> maximal_ranks(const TT& t);
+bool exceeds_maximal_ranks(const TT& t);
+
+// relative downward shift of the certifying Cholesky factorisations (see tt.hip, round_chain)
+constexpr double kGramShift = 1e-11;
+constexpr double kOrthTol = 1e-13;   // max |C_k C_k^T - I| accepted for the right-canonical cores
+
+// Gram chains (k = 1..d-1): left G_{k+1} = M_k^T (G_k M_k), right H_k = M_k (I (x) H_{k+1}) M_k^T
+void left_gram_step(TT& t, std::vector<double*>& G, double* T, size_t k, bool do_reduce = true);
+void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool do_reduce = true);
+void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left = true);
+
+struct DevIdArgs {
+    const double* G[64];
+    int n[64];
+    double* out;
+};
+// max |G_i - I| of a batch of square matrices; out[i * gridDim.y + slice]
+__global__ void k_dev_identity_many(const DevIdArgs args);
+
+// Independent GEMMs; the ones of identical shape go out as one batched launch.
+struct GemmJob {
+    size_t M, N, K, lda, ldb;
+    bool ta, tb;
+    const double* A;
+    const double* B;
+    double* C;
+    bool sym = false;   // result known symmetric (M == N): lower tiles only, mirrored
+    double alpha = 1.0;
+};
+void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs);
+
+// Cholesky (+ explicit inverse) of 256 < n <= 512 matrices from the n <= 256 kernels (2 x 2 blocks)
+constexpr int kBigMax = 64;
+struct BigJob {
+    const double* src;
+    double shift_rel;
+    int n;
+    double* L;   // factor jobs: full L and Z = L^{-1} (n x n); certificates: both null
+    double* Z;
+};
+void factor_big(xrs_handle_t h, const std::vector<BigJob>& jobs, int* status, std::vector<DevBuf>& keep);
+
+// the reference's two-sweep algorithm pieces (sequential, host-synchronising)
+void transfer_right(TT& t, size_t k, bool rank_reduce);   // transfer_core(k -> k+1): QC (or QR) + R * next
+void orth_right(TT& t, size_t k);
+size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps);
+void truncate_edge(TT& t, size_t k, size_t max_rank, double eps);
+
+// certified truncating round (tt_trunc.hip): left-canonical chain pass + device-resident right-to-left
+// truncation sweep with one host synchronisation; false (cores untouched) when a certificate fails
+bool round_truncate(TT& t, const size_t* max_ranks, double eps);
+
+}  // namespace ttd
+}  // namespace xrs

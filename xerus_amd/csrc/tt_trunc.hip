@@ -1,0 +1,322 @@
+// Certified truncating TT round: TTNetwork::round (ttNetwork.cpp:644-665) when ranks are cut.
+//
+// The reference: canonicalize_right (pivoted-QR sweep left to right, rank rule |R_kk| < 16 eps R_00),
+// then right to left round_edge per edge (tensorNetwork.cpp:678-818): SVD of the edge's r x r factor,
+// cut at maxRank then at the first sigma_j <= eps sigma_0 (tensor.cpp:1462-1474), core k <- Vt, core
+// k-1 <- core k-1 * U S. Here, for a TT whose unfoldings are provably well conditioned:
+//  1. structural rank excess at the left end (r_{k+1} > n_0 ... n_k, e.g. after x + y) is removed by
+//     the reference's own QC steps (exact rank rule), then one left chain pass gives the left-canonical
+//     cores: G_{k+1} = M_k^T (G_k (x) I) M_k, G_k = L_k L_k^T, A_k = (L_k^T (x) I) M_k L_{k+1}^{-T}, with
+//     a status-only Cholesky of G_k - tau tr(G_k) I per edge certifying that no QC rank drop happens;
+//  2. the right-to-left sweep runs on the device without host synchronisation: per edge the Gram P of
+//     the edge matrix B (r x N: P = B B^T, or B^T B when r > N), its Cholesky factor L (plus the
+//     certificate chol(P - tau tr(P) I): sigma_min(B) >= sqrt(tau/2) ||B||_F > eps sigma_0, so the eps
+//     rule cannot cut and the rank is min(r, N, maxRank) -- known on the host in advance), the right
+//     singular vectors of L (or L^T) by one-sided Jacobi in LDS (svd.hip), and three GEMMs:
+//        wide (B = L Q):    core_k <- Vt_kk L^{-1} B,  core_{k-1} <- core_{k-1} (L Vt_kk^T)
+//        tall (B = Q L^T):  core_k <- Vt_kk,           core_{k-1} <- core_{k-1} (B Vt_kk^T);
+//  3. one host synchronisation reads every status (factorisations, Jacobi convergence) and the
+//     orthonormality of the left-canonical and of the final right-canonical cores. Any failure discards
+//     the new cores and the caller runs the reference's algorithm (tt.hip: orth_right + truncate_edge).
+// Same ranks and the same singular values as the reference; the kept subspaces and hence the
+// represented tensor agree up to rounding (the SVD gauge of the cores may differ, as for every SVD).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+
+#include "tt_common.hpp"
+
+namespace xrs {
+namespace ttd {
+
+namespace {
+
+constexpr double kTruncOrthTol = 1e-12;   // max |C C^T - I| accepted for the new cores
+
+// Host-side record of everything enqueued; buffers are released once the sweep is judged.
+struct Sweep {
+    TT& t;
+    std::vector<DevBuf> keep;
+    std::vector<double*> owned;   // pool blocks that become cores on success (released on failure)
+    explicit Sweep(TT& tt) : t(tt) {}
+    double* buf(size_t elems) {
+        keep.emplace_back(t.h, std::max<size_t>(elems, 1) * 8);
+        return keep.back().d();
+    }
+    double* core(size_t elems) {
+        double* p = t.alloc(elems);
+        owned.push_back(p);
+        return p;
+    }
+    void drop(double* p) {   // a core block that is no longer needed
+        auto it = std::find(owned.begin(), owned.end(), p);
+        if (it != owned.end()) {
+            owned.erase(it);
+            t.release(p);
+        }
+    }
+    void discard() {
+        for (double* p : owned) t.release(p);
+        owned.clear();
+    }
+};
+
+// one or more Cholesky factorisations of an n x n symmetric matrix in a single launch (n <= 512):
+// the factor L (lower, out of place) and its inverse Z = L^{-1}, plus status-only certificates
+// chol(A - tau tr(A) I). Statuses go to status[0..count).
+struct CholJob {
+    const double* A;
+    int n;
+    double* L;   // null: certificate only
+    double* Z;
+};
+
+void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
+    xrs_handle_t h = sw.t.h;
+    std::vector<BigJob> big;
+    std::vector<int> big_slot;
+    PotrfBatch pb{};
+    TrinvBatch tb{};
+    int ns = 0, ninv = 0;
+    for (size_t i = 0; i < jobs.size(); ++i) {
+        const CholJob& j = jobs[i];
+        if (j.n > 256) {
+            big.push_back({j.A, j.L ? 0.0 : -kGramShift, j.n, j.L, j.Z});
+            big_slot.push_back(int(i));
+            continue;
+        }
+        XRS_REQUIRE(ns < kPotrfBatchMax, "chol_jobs: batch too large");
+        double* dinv = j.L ? sw.buf(dinv_elems(j.n)) : sw.buf(dinv_elems(j.n));
+        pb.src[ns] = j.A;
+        pb.G[ns] = j.L;
+        pb.Dinv[ns] = dinv;
+        pb.shift[ns] = j.L ? 0.0 : -kGramShift;
+        pb.n[ns] = j.n;
+        ++ns;
+        if (j.L) {
+            tb.L[ninv] = j.L;
+            tb.Dinv[ninv] = dinv;
+            tb.X[ninv] = j.Z;
+            tb.n[ninv] = j.n;
+            ++ninv;
+        }
+    }
+    // statuses: the small jobs first in job order is not needed -- keep one slot per small job, then two
+    // per big job (factor_big's two diagonal blocks); the caller only tests all-zero
+    if (ns) {
+        pb.status = status;
+        potrf_batched(h, pb, ns);
+    }
+    if (ninv) trinv_batched(h, tb, ninv);
+    if (!big.empty()) {
+        std::vector<DevBuf> keep;
+        factor_big(h, big, status + ns, keep);
+        for (auto& k : keep) sw.keep.push_back(std::move(k));
+    }
+}
+
+int chol_status_count(const std::vector<CholJob>& jobs) {
+    int c = 0;
+    for (const CholJob& j : jobs) c += j.n > 256 ? 2 : 1;
+    return c;
+}
+
+// max |X X^T - I| (rows, `rows` = true) or max |X^T X - I| of a list of matrices -> dev[0..count*16)
+void orth_devs(Sweep& sw, const std::vector<const double*>& X, const std::vector<size_t>& m, const std::vector<size_t>& n,
+               bool rows, double* dev) {
+    xrs_handle_t h = sw.t.h;
+    const size_t cnt = X.size();
+    std::vector<GemmJob> grams;
+    DevIdArgs da{};
+    for (size_t i = 0; i < cnt; ++i) {
+        const size_t g = rows ? m[i] : n[i];
+        double* G = sw.buf(g * g);
+        if (rows) grams.push_back({g, g, n[i], n[i], n[i], false, true, X[i], X[i], G, true});
+        else grams.push_back({g, g, m[i], g, g, true, false, X[i], X[i], G, true});
+        da.G[i] = G;
+        da.n[i] = int(g);
+    }
+    gemm_grouped(h, grams);
+    da.out = dev;
+    hipLaunchKernelGGL(k_dev_identity_many, dim3(unsigned(cnt), 16), dim3(256), 0, h->stream, da);
+    check_launch("k_dev_identity_many");
+}
+
+}  // namespace
+
+bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
+    if (d < 2 || d > 64 || t.sharded()) return false;
+    const double cX = 0.5 * std::sqrt(kGramShift);
+    if (!(eps < 0.25 * cX * cX)) return false;
+    for (size_t k = 1; k < d; ++k)
+        if (t.r[k] > size_t(kSmallMax)) return false;
+
+    // 1a. structural excess (a wide left unfolding, r_{k+1} > r_k n_k, e.g. the boundary edges of x + y):
+    //     the reference's own QC steps there (exact rank rule, host syncs)
+    for (size_t k = 0; k + 1 < d; ++k)
+        if (t.r[k + 1] > t.r[k] * t.n[k]) transfer_right(t, k, true);
+
+    Sweep sw(t);
+    // statuses: factorisations from 0 up, Jacobi convergence at kJacobiSlot + edge
+    constexpr int kStatusWords = 1024, kJacobiSlot = 768;
+    DevBuf st(h, kStatusWords * 4), devb(h, 64 * 16 * 8);
+    int* status = st.as<int>();
+    int nst = 0;
+    XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
+
+    // 1b. left chain pass: G_k (k = 1..d-1) on the main stream
+    std::vector<double*> G(d, nullptr);
+    size_t tmax = 1;
+    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
+    double* T = sw.buf(tmax);
+    for (size_t k = 1; k < d; ++k) G[k] = sw.buf(t.r[k] * t.r[k]);
+    for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, T, k, false);
+    std::vector<double*> Lf(d, nullptr), Zf(d, nullptr);
+    std::vector<CholJob> jobs;
+    for (size_t k = 1; k < d; ++k) {
+        const int a = int(t.r[k]);
+        Lf[k] = sw.buf(size_t(a) * a);
+        Zf[k] = sw.buf(size_t(a) * a);
+        jobs.push_back({G[k], a, Lf[k], Zf[k]});
+        jobs.push_back({G[k], a, nullptr, nullptr});
+    }
+    for (size_t b0 = 0; b0 < jobs.size(); b0 += 40) {   // (potrf_batched / trinv tables hold 48 / 64)
+        const std::vector<CholJob> part(jobs.begin() + long(b0), jobs.begin() + long(std::min(jobs.size(), b0 + 40)));
+        chol_jobs(sw, part, status + nst);
+        nst += chol_status_count(part);
+    }
+    // A_k = (L_k^T (x) I) M_k Z_{k+1}^T; the left factor as one GEMM on the r_k x (n_k r_{k+1}) unfolding
+    std::vector<double*> A(d, nullptr), W(d, nullptr);
+    std::vector<GemmJob> lefts, rights;
+    for (size_t k = 0; k < d; ++k) {
+        A[k] = sw.core(t.size(k));
+        if (k == 0) continue;
+        const size_t a = t.r[k], cols = t.cols_right(k);
+        W[k] = (k + 1 < d) ? sw.buf(t.size(k)) : A[k];
+        lefts.push_back({a, cols, a, a, cols, true, false, Lf[k], t.core[k], W[k]});
+    }
+    for (size_t k = 0; k + 1 < d; ++k) {
+        const size_t b = t.r[k + 1];
+        rights.push_back({t.rows_left(k), b, b, b, b, false, true, k == 0 ? t.core[0] : W[k], Zf[k + 1], A[k]});
+    }
+    gemm_grouped(h, lefts);
+    gemm_grouped(h, rights);
+    // left-orthonormality of A_0 .. A_{d-2}
+    {
+        std::vector<const double*> X;
+        std::vector<size_t> m, n;
+        for (size_t k = 0; k + 1 < d; ++k) {
+            X.push_back(A[k]);
+            m.push_back(t.rows_left(k));
+            n.push_back(t.r[k + 1]);
+        }
+        orth_devs(sw, X, m, n, false, devb.d());
+    }
+    // check point 1 (one host sync): the certificates and the left-canonical form
+    int* hs = static_cast<int*>(h->host_scratch) + 13312;
+    double* hd = static_cast<double*>(h->host_scratch) + 2048;
+    const int nchk1 = int(d - 1) * 16;
+    XRS_HIP(hipMemcpyAsync(hs, status, size_t(nst) * 4, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk1) * 8, hipMemcpyDeviceToHost, h->stream));
+    host_wait(h);
+    {
+        bool ok = true;
+        for (int i = 0; i < nst; ++i) ok = ok && hs[i] == 0;
+        double worst = 0.0;
+        for (int i = 0; i < nchk1; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
+        if (!ok || !(worst <= kTruncOrthTol)) {
+            if (dbg) std::fprintf(stderr, "round_truncate: left pass %s, orthogonality %.3e -> reference path\n",
+                                  ok ? "certified" : "NOT certified", worst);
+            sw.discard();
+            return false;
+        }
+    }
+
+    // 2. right-to-left truncation sweep, device resident; new ranks decided on the host in advance
+    std::vector<size_t> rr(t.r, t.r + d + 1);   // ranks as the sweep goes
+    nst = 0;
+    XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
+    std::vector<int*> jst;   // Jacobi statuses
+    for (size_t k = d - 1; k >= 1; --k) {
+        const size_t r = rr[k], N = t.n[k] * rr[k + 1];
+        const size_t kk = std::min({r, N, max_ranks[k - 1]});
+        const bool wide = r <= N;
+        const size_t g = wide ? r : N;
+        double* B = A[k];
+        double* P = sw.buf(g * g);
+        if (wide) gemm_sym(h, P, g, 1.0, B, N, false, N, B, N, true);
+        else gemm_sym(h, P, g, 1.0, B, N, true, r, B, N, false);
+        double* L = sw.buf(g * g);
+        double* Z = sw.buf(g * g);
+        const std::vector<CholJob> cj{{P, int(g), L, Z}, {P, int(g), nullptr, nullptr}};
+        chol_jobs(sw, cj, status + nst);
+        nst += chol_status_count(cj);
+        double* S = sw.buf(g);
+        double* Vt = wide ? sw.buf(g * g) : sw.core(g * g);
+        int* js = status + kJacobiSlot + int(jst.size());
+        jacobi_vt(h, L, int(g), !wide, int(g), int(g), S, Vt, int(g), js);
+        jst.push_back(js);
+        double* Tk = sw.buf(r * kk);
+        double* newk;
+        if (wide) {
+            double* M = sw.buf(kk * r);
+            gemm(h, M, kk, r, 1.0, Vt, r, false, r, Z, r, false);                 // Vt_kk L^{-1}
+            newk = sw.core(kk * N);
+            gemm(h, newk, kk, N, 1.0, M, r, false, r, B, N, false);               // Vt_kk Q
+            gemm(h, Tk, r, kk, 1.0, L, r, false, r, Vt, r, true);                 // U S = L Vt_kk^T
+        } else {
+            newk = Vt;                                                            // first kk rows
+            gemm(h, Tk, r, kk, 1.0, B, N, false, N, Vt, N, true);                 // U S = B Vt_kk^T
+        }
+        const size_t prow = t.rows_left(k - 1);   // = rr[k-1] * n[k-1] (left ranks unchanged so far)
+        double* prevk = sw.core(prow * kk);
+        gemm(h, prevk, prow, kk, 1.0, A[k - 1], r, false, r, Tk, kk, false);
+        sw.drop(B);
+        sw.drop(A[k - 1]);
+        A[k] = newk;
+        A[k - 1] = prevk;
+        rr[k] = kk;
+    }
+    // right-orthonormality of the new cores 1..d-1
+    {
+        std::vector<const double*> X;
+        std::vector<size_t> m, n;
+        for (size_t k = 1; k < d; ++k) {
+            X.push_back(A[k]);
+            m.push_back(rr[k]);
+            n.push_back(t.n[k] * rr[k + 1]);
+        }
+        orth_devs(sw, X, m, n, true, devb.d());
+    }
+    const int nchk2 = int(d - 1) * 16;
+    XRS_HIP(hipMemcpyAsync(hs, status, size_t(kStatusWords) * 4, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk2) * 8, hipMemcpyDeviceToHost, h->stream));
+    host_wait(h);
+    bool ok = true;
+    for (int i = 0; i < nst; ++i) ok = ok && hs[i] == 0;
+    int max_sweeps = 0;
+    for (size_t i = 0; i < jst.size(); ++i) {
+        const int s = hs[kJacobiSlot + int(i)];
+        ok = ok && s >= 0;
+        max_sweeps = std::max(max_sweeps, s);
+    }
+    double worst = 0.0;
+    for (int i = 0; i < nchk2; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
+    if (dbg) std::fprintf(stderr, "round_truncate: sweep %s, max Jacobi sweeps %d, orthogonality %.3e\n",
+                          ok ? "certified" : "NOT certified", max_sweeps, worst);
+    if (!ok || !(worst <= kTruncOrthTol)) {
+        sw.discard();
+        return false;
+    }
+    for (size_t k = 0; k < d; ++k) t.replace(k, A[k]);
+    sw.owned.clear();
+    for (size_t k = 1; k < d; ++k) t.r[k] = rr[k];
+    return true;
+}
+
+}  // namespace ttd
+}  // namespace xrs
