@@ -1,0 +1,32 @@
+"""Truncating-round timing probe (diagnostics): cfg3 round(64) and (x+y).round(128) a few times.
+
+Run under rocprofv3 --kernel-trace --stats on the GPU box to see where a truncating round goes."""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import xerus_amd.xerus as xe  # noqa: E402
+from xerus_amd import capi  # noqa: E402
+
+h = capi.Handle(0)
+d, n, r = 10, 20, int(os.environ.get("RANK", "128"))
+target = int(os.environ.get("TARGET", "64"))
+reps = int(os.environ.get("REPS", "5"))
+ranks = bench.tt_ranks(d, n, r)
+x = capi.TTDevice.from_cores(h, bench.random_cores(xe, [n] * d, ranks, bench.SEED + 11))
+x.move_core(0)
+for i in range(reps):
+    c = x.clone()
+    h.synchronize()
+    t0 = time.perf_counter()
+    c.round(target)
+    h.synchronize()
+    print(f"round({target}) of rank {r}: {(time.perf_counter() - t0) * 1e3:.3f} ms path={h.last_round_path()} ranks={c.ranks}",
+          flush=True)
+    c.free()

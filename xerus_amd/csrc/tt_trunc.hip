@@ -13,8 +13,9 @@
 //     certificate chol(P - tau tr(P) I): sigma_min(B) >= sqrt(tau/2) ||B||_F > eps sigma_0, so the eps
 //     rule cannot cut and the rank is min(r, N, maxRank) -- known on the host in advance), the right
 //     singular vectors of L (or L^T) by one-sided Jacobi in LDS (svd.hip), and three GEMMs:
-//        wide (B = L Q):    core_k <- Vt_kk L^{-1} B,  core_{k-1} <- core_{k-1} (L Vt_kk^T)
-//        tall (B = Q L^T):  core_k <- Vt_kk,           core_{k-1} <- core_{k-1} (B Vt_kk^T);
+//        wide (B = L Q, L = U S V^T): core_k <- S_kk^{-1} U_kk^T B,  core_{k-1} <- core_{k-1} (U S)_kk
+//        tall (B = Q L^T):            core_k <- Vt_kk,               core_{k-1} <- core_{k-1} (B Vt_kk^T)
+//     (the Jacobi runs on the columns of L in both cases: U of L in the wide, Vt of L^T in the tall case);
 //  3. one host synchronisation reads every status (factorisations, Jacobi convergence) and the
 //     orthonormality of the left-canonical and of the final right-canonical cores. Any failure discards
 //     the new cores and the caller runs the reference's algorithm (tt.hip: orth_right + truncate_edge).
@@ -94,7 +95,7 @@ void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
         pb.shift[ns] = j.L ? 0.0 : -kGramShift;
         pb.n[ns] = j.n;
         ++ns;
-        if (j.L) {
+        if (j.L && j.Z) {
             tb.L[ninv] = j.L;
             tb.Dinv[ninv] = dinv;
             tb.X[ninv] = j.Z;
@@ -143,6 +144,64 @@ void orth_devs(Sweep& sw, const std::vector<const double*>& X, const std::vector
     check_launch("k_dev_identity_many");
 }
 
+// wide edge, B = L Q with the left singular vectors of L as the rows of Ut (Jacobi on the columns of L):
+// M = S^{-1} Ut[:kk] (new core = M B = Vt_kk Q) and T = Ut[:kk]^T S (= U S, core_{k-1} <- core_{k-1} T)
+__global__ void __launch_bounds__(256) k_edge_factors(const double* __restrict__ Ut, const double* __restrict__ S, int r, int kk,
+                                                      double* __restrict__ M, double* __restrict__ T) {
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < kk * r; e += gridDim.x * 256) {
+        const int i = e / r, j = e - i * r;
+        const double u = Ut[size_t(i) * r + j], s = S[i];
+        M[e] = s > 0.0 ? u / s : 0.0;
+        T[size_t(j) * kk + i] = u * s;
+    }
+}
+
+// One left chain pass over the cores `src` (ranks t.r): G_{k+1} = M_k^T (G_k (x) I) M_k, G_k = L_k L_k^T
+// (+ the status-only certificate of G_k - tau tr(G_k) I with `certify`), Z_k = L_k^{-1}, and the
+// left-canonical cores A_k = (L_k^T (x) I) M_k Z_{k+1}^T (A_{d-1} = (L^T (x) I) M_{d-1}).
+void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<double*>& A, int* status, int& nst) {
+    TT t = t0;
+    t.core = const_cast<double**>(src);
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    std::vector<double*> G(d, nullptr);
+    size_t tmax = 1;
+    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
+    double* T = sw.buf(tmax);
+    for (size_t k = 1; k < d; ++k) G[k] = sw.buf(t.r[k] * t.r[k]);
+    for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, T, k, false);
+    std::vector<double*> Lf(d, nullptr), Zf(d, nullptr);
+    std::vector<CholJob> jobs;
+    for (size_t k = 1; k < d; ++k) {
+        const int a = int(t.r[k]);
+        Lf[k] = sw.buf(size_t(a) * a);
+        Zf[k] = sw.buf(size_t(a) * a);
+        jobs.push_back({G[k], a, Lf[k], Zf[k]});
+        if (certify) jobs.push_back({G[k], a, nullptr, nullptr});
+    }
+    for (size_t b0 = 0; b0 < jobs.size(); b0 += 40) {   // (potrf_batched / trinv tables hold 48 / 64)
+        const std::vector<CholJob> part(jobs.begin() + long(b0), jobs.begin() + long(std::min(jobs.size(), b0 + 40)));
+        chol_jobs(sw, part, status + nst);
+        nst += chol_status_count(part);
+    }
+    A.assign(d, nullptr);
+    std::vector<double*> W(d, nullptr);
+    std::vector<GemmJob> lefts, rights;
+    for (size_t k = 0; k < d; ++k) {
+        A[k] = sw.core(t.size(k));
+        if (k == 0) continue;
+        const size_t a = t.r[k], cols = t.cols_right(k);
+        W[k] = (k + 1 < d) ? sw.buf(t.size(k)) : A[k];
+        lefts.push_back({a, cols, a, a, cols, true, false, Lf[k], t.core[k], W[k]});
+    }
+    for (size_t k = 0; k + 1 < d; ++k) {
+        const size_t b = t.r[k + 1];
+        rights.push_back({t.rows_left(k), b, b, b, b, false, true, k == 0 ? t.core[0] : W[k], Zf[k + 1], A[k]});
+    }
+    gemm_grouped(h, lefts);
+    gemm_grouped(h, rights);
+}
+
 }  // namespace
 
 bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
@@ -168,72 +227,49 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     int nst = 0;
     XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
 
-    // 1b. left chain pass: G_k (k = 1..d-1) on the main stream
-    std::vector<double*> G(d, nullptr);
-    size_t tmax = 1;
-    for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
-    double* T = sw.buf(tmax);
-    for (size_t k = 1; k < d; ++k) G[k] = sw.buf(t.r[k] * t.r[k]);
-    for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, T, k, false);
-    std::vector<double*> Lf(d, nullptr), Zf(d, nullptr);
-    std::vector<CholJob> jobs;
-    for (size_t k = 1; k < d; ++k) {
-        const int a = int(t.r[k]);
-        Lf[k] = sw.buf(size_t(a) * a);
-        Zf[k] = sw.buf(size_t(a) * a);
-        jobs.push_back({G[k], a, Lf[k], Zf[k]});
-        jobs.push_back({G[k], a, nullptr, nullptr});
-    }
-    for (size_t b0 = 0; b0 < jobs.size(); b0 += 40) {   // (potrf_batched / trinv tables hold 48 / 64)
-        const std::vector<CholJob> part(jobs.begin() + long(b0), jobs.begin() + long(std::min(jobs.size(), b0 + 40)));
-        chol_jobs(sw, part, status + nst);
-        nst += chol_status_count(part);
-    }
-    // A_k = (L_k^T (x) I) M_k Z_{k+1}^T; the left factor as one GEMM on the r_k x (n_k r_{k+1}) unfolding
-    std::vector<double*> A(d, nullptr), W(d, nullptr);
-    std::vector<GemmJob> lefts, rights;
-    for (size_t k = 0; k < d; ++k) {
-        A[k] = sw.core(t.size(k));
-        if (k == 0) continue;
-        const size_t a = t.r[k], cols = t.cols_right(k);
-        W[k] = (k + 1 < d) ? sw.buf(t.size(k)) : A[k];
-        lefts.push_back({a, cols, a, a, cols, true, false, Lf[k], t.core[k], W[k]});
-    }
-    for (size_t k = 0; k + 1 < d; ++k) {
-        const size_t b = t.r[k + 1];
-        rights.push_back({t.rows_left(k), b, b, b, b, false, true, k == 0 ? t.core[0] : W[k], Zf[k + 1], A[k]});
-    }
-    gemm_grouped(h, lefts);
-    gemm_grouped(h, rights);
-    // left-orthonormality of A_0 .. A_{d-2}
-    {
-        std::vector<const double*> X;
-        std::vector<size_t> m, n;
-        for (size_t k = 0; k + 1 < d; ++k) {
-            X.push_back(A[k]);
-            m.push_back(t.rows_left(k));
-            n.push_back(t.r[k + 1]);
-        }
-        orth_devs(sw, X, m, n, false, devb.d());
-    }
-    // check point 1 (one host sync): the certificates and the left-canonical form
+    // 1b. left chain pass (certified), and a second one on its output when a single CholeskyQR pass over
+    //     the train left the cores short of orthonormal (kappa^2 u > tol: CholeskyQR2 on the whole train)
     int* hs = static_cast<int*>(h->host_scratch) + 13312;
     double* hd = static_cast<double*>(h->host_scratch) + 2048;
-    const int nchk1 = int(d - 1) * 16;
-    XRS_HIP(hipMemcpyAsync(hs, status, size_t(nst) * 4, hipMemcpyDeviceToHost, h->stream));
-    XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk1) * 8, hipMemcpyDeviceToHost, h->stream));
-    host_wait(h);
-    {
+    std::vector<double*> A;
+    left_pass(sw, t, t.core, true, A, status, nst);
+    double worst = 0.0;
+    for (int pass = 1;; ++pass) {
+        {
+            std::vector<const double*> X;
+            std::vector<size_t> m, n;
+            for (size_t k = 0; k + 1 < d; ++k) {
+                X.push_back(A[k]);
+                m.push_back(t.rows_left(k));
+                n.push_back(t.r[k + 1]);
+            }
+            orth_devs(sw, X, m, n, false, devb.d());
+        }
+        // check point (one host sync): the factorisations and the left-canonical form
+        const int nchk = int(d - 1) * 16;
+        XRS_HIP(hipMemcpyAsync(hs, status, size_t(nst) * 4, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
+        host_wait(h);
         bool ok = true;
         for (int i = 0; i < nst; ++i) ok = ok && hs[i] == 0;
-        double worst = 0.0;
-        for (int i = 0; i < nchk1; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
-        if (!ok || !(worst <= kTruncOrthTol)) {
-            if (dbg) std::fprintf(stderr, "round_truncate: left pass %s, orthogonality %.3e -> reference path\n",
-                                  ok ? "certified" : "NOT certified", worst);
+        worst = 0.0;
+        for (int i = 0; i < nchk; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
+        if (dbg) std::fprintf(stderr, "round_truncate: left pass %d %s, orthogonality %.3e\n", pass,
+                              ok ? "certified" : "NOT certified", worst);
+        if (!ok) {
             sw.discard();
             return false;
         }
+        if (worst <= kTruncOrthTol) break;
+        if (pass == 2) {
+            sw.discard();
+            return false;
+        }
+        std::vector<double*> A1 = A;
+        nst = 0;
+        XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
+        left_pass(sw, t, A1.data(), false, A, status, nst);
+        for (double* p : A1) sw.drop(p);
     }
 
     // 2. right-to-left truncation sweep, device resident; new ranks decided on the host in advance
@@ -251,24 +287,27 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         if (wide) gemm_sym(h, P, g, 1.0, B, N, false, N, B, N, true);
         else gemm_sym(h, P, g, 1.0, B, N, true, r, B, N, false);
         double* L = sw.buf(g * g);
-        double* Z = sw.buf(g * g);
+        double* Z = g > 256 ? sw.buf(g * g) : nullptr;   // (factor_big always builds L^{-1})
         const std::vector<CholJob> cj{{P, int(g), L, Z}, {P, int(g), nullptr, nullptr}};
         chol_jobs(sw, cj, status + nst);
         nst += chol_status_count(cj);
+        // one-sided Jacobi on the rows of L^T, i.e. on the columns of the Cholesky factor (Drmac-Veselic:
+        // the triangular factor's transpose converges in far fewer sweeps than the factor itself)
         double* S = sw.buf(g);
         double* Vt = wide ? sw.buf(g * g) : sw.core(g * g);
         int* js = status + kJacobiSlot + int(jst.size());
-        jacobi_vt(h, L, int(g), !wide, int(g), int(g), S, Vt, int(g), js);
+        jacobi_vt(h, L, int(g), true, int(g), int(g), S, Vt, int(g), js);
         jst.push_back(js);
         double* Tk = sw.buf(r * kk);
         double* newk;
-        if (wide) {
+        if (wide) {   // Vt holds U_L^T (P = B B^T = L L^T, B = L Q, L = U S V^T)
             double* M = sw.buf(kk * r);
-            gemm(h, M, kk, r, 1.0, Vt, r, false, r, Z, r, false);                 // Vt_kk L^{-1}
+            hipLaunchKernelGGL(k_edge_factors, dim3(unsigned(std::min<size_t>((kk * r + 255) / 256, 512))), dim3(256), 0,
+                               h->stream, Vt, S, int(r), int(kk), M, Tk);
+            check_launch("k_edge_factors");
             newk = sw.core(kk * N);
-            gemm(h, newk, kk, N, 1.0, M, r, false, r, B, N, false);               // Vt_kk Q
-            gemm(h, Tk, r, kk, 1.0, L, r, false, r, Vt, r, true);                 // U S = L Vt_kk^T
-        } else {
+            gemm(h, newk, kk, N, 1.0, M, r, false, r, B, N, false);               // S^{-1} U^T B = Vt_B[:kk]
+        } else {      // Vt holds the right singular vectors of L^T = those of B (B = Q L^T)
             newk = Vt;                                                            // first kk rows
             gemm(h, Tk, r, kk, 1.0, B, N, false, N, Vt, N, true);                 // U S = B Vt_kk^T
         }
@@ -304,7 +343,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         ok = ok && s >= 0;
         max_sweeps = std::max(max_sweeps, s);
     }
-    double worst = 0.0;
+    worst = 0.0;
     for (int i = 0; i < nchk2; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
     if (dbg) std::fprintf(stderr, "round_truncate: sweep %s, max Jacobi sweeps %d, orthogonality %.3e\n",
                           ok ? "certified" : "NOT certified", max_sweeps, worst);
