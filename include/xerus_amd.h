@@ -163,6 +163,19 @@ int xrs_tt_dot(xrs_handle_t handle, double* result, size_t d, const size_t* n,
  *  A NULL hook means one rank: the local sums are final and no synchronisation happens. */
 typedef int (*xrs_allreduce_fn)(void* ctx, double* buf, size_t count);
 
+/** RCCL communicator (no reference counterpart: xerus is single-process). xrs_comm_allreduce is an
+ *  xrs_allreduce_fn taking an xrs_comm_t as ctx: it enqueues an in-place fp64 sum ncclAllReduce on the
+ *  handle's stream and returns at once; the sharded TT drivers recognise it and skip the host stream
+ *  synchronisation other hooks need (no host round trip per collective). One rank calls
+ *  xrs_comm_unique_id (128 bytes), the caller distributes the id, every rank calls xrs_comm_create.
+ *  RCCL is loaded at run time; the calls fail with a status if it is absent. */
+typedef struct xrs_comm_s* xrs_comm_t;
+int xrs_comm_unique_id(void* id128_out);
+int xrs_comm_create(xrs_handle_t handle, int nranks, int rank, const void* id128, xrs_comm_t* comm_out);
+int xrs_comm_destroy(xrs_comm_t comm);
+size_t xrs_comm_calls(xrs_comm_t comm);
+int xrs_comm_allreduce(void* comm, double* buf, size_t count);
+
 /** Mode-sharded TT round (no reference counterpart: xerus is single-process).
  *  Each rank holds, for every component k, the mode slices of its own subset (n_local[k] of them) as
  *  an (r_k, n_local[k], r_{k+1}) row-major device array. The Gram chains are sums over the mode index,

@@ -36,7 +36,7 @@ def _rel_diff(ref, a_cores, b_cores):
     return D.frob_norm() / B.frob_norm()
 
 
-def _worker(rank, world, port, backend, force, out):
+def _worker(rank, world, port, backend, hook, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group(backend, rank=rank, world_size=world)
     try:
@@ -46,7 +46,8 @@ def _worker(rank, world, port, backend, force, out):
 
         torch.cuda.set_device(0)
         h = capi.Handle(0)
-        comm = xd.TorchAllReduce(force_hook=force)
+        comm = xd.RcclComm(h) if hook == "rccl" else xd.TorchAllReduce(force_hook=(hook == "force"))
+        force = hook != "none"
         dims, ranks = [8, 6, 7, 5, 8, 6], [6, 12, 12, 10, 6]
         x = ref.TT.random_raw(dims, ranks, ref.Rng(31))
         y = ref.TT.random_raw(dims, ranks, ref.Rng(37))
@@ -81,6 +82,19 @@ def _worker(rank, world, port, backend, force, out):
         res["cert_sum"] = ss.round(100, comm)
         after = ss.local.cores()
         res["untouched"] = all(np.array_equal(a, b) for a, b in zip(before, after))
+        # truncating sharded round (ranks 12 -> 8): the certified truncation with all-reduced Grams
+        st = xd.ShardedTT.from_full_cores(h, x.cores, world, rank)
+        res["cert_trunc"] = st.round(8, comm)
+        full_t = st.gather(dist.all_gather_object)
+        res["trunc_ranks"] = st.ranks
+        if rank == 0:
+            from ttutil import tt_diff_norm
+            xo = x.copy()
+            xo.round(8)
+            res["trunc_ref_ranks"] = xo.ranks
+            e_gpu, nrm = tt_diff_norm(full_t, x.cores)
+            e_ref, _ = tt_diff_norm(xo.cores, x.cores)
+            res["trunc_err_diff"] = abs(e_gpu - e_ref) / nrm
         res["calls"] = comm.calls
         res["device_native"] = comm.device_native
         if force:   # the same work with no hook (one rank): identical results
@@ -97,11 +111,14 @@ def _worker(rank, world, port, backend, force, out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,backend,force", [(2, "gloo", False), (1, "nccl", True)])
-def test_sharded_round_and_dot(world, backend, force):
+@pytest.mark.parametrize("world,backend,hook", [(2, "gloo", "none"), (1, "nccl", "force"), (1, "nccl", "rccl")])
+def test_sharded_round_and_dot(world, backend, hook):
+    """hook: "none" (torch.distributed callback; a NULL hook at world 1), "force" (the callback even at world
+    1: dist.all_reduce on the device buffer), "rccl" (xrs_comm_allreduce: C++ RCCL, stream-ordered)."""
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_worker, args=(world, _free_port(), backend, force, out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), backend, hook, out), nprocs=world, join=True)
+    force = hook != "none"
     r0 = out[0]
     for rank in range(world):
         r = out[rank]
@@ -113,6 +130,10 @@ def test_sharded_round_and_dot(world, backend, force):
     assert r0["diff"] <= 1e-12
     assert r0["orth"] <= 1e-13
     assert r0["calls"] > 0
+    for rank in range(world):
+        assert out[rank]["cert_trunc"] is True
+        assert out[rank]["trunc_ranks"] == r0["trunc_ref_ranks"]
+    assert r0["trunc_err_diff"] <= 1e-6
     if force:
         assert r0["device_native"] is True
         assert r0["dot_null_diff"] <= 1e-15

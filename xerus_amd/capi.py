@@ -60,6 +60,11 @@ SIGNATURES = {
     "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                      C.POINTER(_SZ), C.POINTER(_DP), _DP, _DP]),
     "xrs_tt_last_round_path": (C.c_int, [_DP]),
+    "xrs_comm_unique_id": (C.c_int, [_DP]),
+    "xrs_comm_create": (C.c_int, [_DP, C.c_int, C.c_int, _DP, C.POINTER(_DP)]),
+    "xrs_comm_destroy": (C.c_int, [_DP]),
+    "xrs_comm_calls": (_SZ, [_DP]),
+    "xrs_comm_allreduce": (C.c_int, [_DP, _DP, _SZ]),
     "xrs_prof_begin": (C.c_int, [_DP, C.c_uint32]),
     "xrs_prof_end": (C.c_int, [_DP, C.POINTER(_SZ), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                C.POINTER(C.c_double)]),

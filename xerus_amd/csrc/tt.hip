@@ -989,7 +989,8 @@ int xrs_tt_round_sharded(xrs_handle_t h, size_t d, const size_t* n_local, size_t
         t.shard_mode = true;
         t.ar = allreduce;   // null: one rank
         t.ar_ctx = ctx;
-        *certified = round_chain(t, max_ranks, eps) ? 1 : 0;
+        // no cut possible: the chain round; ranks to cut: the certified truncation (wide edges only)
+        *certified = (round_chain(t, max_ranks, eps) || round_truncate(t, max_ranks, eps)) ? 1 : 0;
     });
 }
 

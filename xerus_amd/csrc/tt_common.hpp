@@ -32,7 +32,8 @@ struct TT {
     bool sharded() const { return shard_mode; }
     void reduce(double* buf, size_t count) const {
         if (!ar) return;
-        XRS_HIP(hipStreamSynchronize(h->stream));
+        // the built-in RCCL hook is stream-ordered; any other hook sees a synchronised stream
+        if (ar != &xrs_comm_allreduce) XRS_HIP(hipStreamSynchronize(h->stream));
         const int rc = ar(ar_ctx, buf, count);
         XRS_REQUIRE(rc == 0, "all-reduce callback failed");
     }

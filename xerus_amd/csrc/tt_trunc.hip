@@ -123,22 +123,29 @@ int chol_status_count(const std::vector<CholJob>& jobs) {
     return c;
 }
 
-// max |X X^T - I| (rows, `rows` = true) or max |X^T X - I| of a list of matrices -> dev[0..count*16)
+// max |X X^T - I| (rows, `rows` = true) or max |X^T X - I| of a list of matrices -> dev[0..count*16);
+// the Grams sit in one buffer, completed across ranks by ONE all-reduce when sharded
 void orth_devs(Sweep& sw, const std::vector<const double*>& X, const std::vector<size_t>& m, const std::vector<size_t>& n,
                bool rows, double* dev) {
     xrs_handle_t h = sw.t.h;
     const size_t cnt = X.size();
+    size_t total = 0;
+    for (size_t i = 0; i < cnt; ++i) total += (rows ? m[i] : n[i]) * (rows ? m[i] : n[i]);
+    double* all = sw.buf(total);
     std::vector<GemmJob> grams;
     DevIdArgs da{};
+    size_t off = 0;
     for (size_t i = 0; i < cnt; ++i) {
         const size_t g = rows ? m[i] : n[i];
-        double* G = sw.buf(g * g);
+        double* G = all + off;
+        off += g * g;
         if (rows) grams.push_back({g, g, n[i], n[i], n[i], false, true, X[i], X[i], G, true});
         else grams.push_back({g, g, m[i], g, g, true, false, X[i], X[i], G, true});
         da.G[i] = G;
         da.n[i] = int(g);
     }
     gemm_grouped(h, grams);
+    sw.t.reduce(all, total);
     da.out = dev;
     hipLaunchKernelGGL(k_dev_identity_many, dim3(unsigned(cnt), 16), dim3(256), 0, h->stream, da);
     check_launch("k_dev_identity_many");
@@ -169,7 +176,7 @@ void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<
     for (size_t k = 1; k + 1 < d; ++k) tmax = std::max(tmax, t.size(k));
     double* T = sw.buf(tmax);
     for (size_t k = 1; k < d; ++k) G[k] = sw.buf(t.r[k] * t.r[k]);
-    for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, T, k, false);
+    for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, T, k, true);   // (sharded: + one all-reduce per step)
     std::vector<double*> Lf(d, nullptr), Zf(d, nullptr);
     std::vector<CholJob> jobs;
     for (size_t k = 1; k < d; ++k) {
@@ -208,7 +215,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
     static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
-    if (d < 2 || d > 64 || t.sharded()) return false;
+    if (d < 2 || d > 64) return false;
     const double cX = 0.5 * std::sqrt(kGramShift);
     if (!(eps < 0.25 * cX * cX)) return false;
     for (size_t k = 1; k < d; ++k)
@@ -216,8 +223,11 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
 
     // 1a. structural excess (a wide left unfolding, r_{k+1} > r_k n_k, e.g. the boundary edges of x + y):
     //     the reference's own QC steps there (exact rank rule, host syncs)
-    for (size_t k = 0; k + 1 < d; ++k)
-        if (t.r[k + 1] > t.r[k] * t.n[k]) transfer_right(t, k, true);
+    //     (sharded: not available -- an excess makes the left Gram singular, the certificate fails and the
+    //     caller rounds the gathered TT instead)
+    if (!t.sharded())
+        for (size_t k = 0; k + 1 < d; ++k)
+            if (t.r[k + 1] > t.r[k] * t.n[k]) transfer_right(t, k, true);
 
     Sweep sw(t);
     // statuses: factorisations from 0 up, Jacobi convergence at kJacobiSlot + edge
@@ -226,6 +236,16 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     int* status = st.as<int>();
     int nst = 0;
     XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
+    // global mode sizes (sharded: the sum of every rank's slice counts, read at the first check point)
+    std::vector<size_t> ng(t.n, t.n + d);
+    double* nsum = nullptr;
+    if (t.sharded()) {
+        double* hn = static_cast<double*>(h->host_scratch) + 3400;
+        for (size_t k = 0; k < d; ++k) hn[k] = double(t.n[k]);
+        nsum = sw.buf(d);
+        XRS_HIP(hipMemcpyAsync(nsum, hn, d * 8, hipMemcpyHostToDevice, h->stream));
+        t.reduce(nsum, d);
+    }
 
     // 1b. left chain pass (certified), and a second one on its output when a single CholeskyQR pass over
     //     the train left the cores short of orthonormal (kappa^2 u > tol: CholeskyQR2 on the whole train)
@@ -249,7 +269,10 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         const int nchk = int(d - 1) * 16;
         XRS_HIP(hipMemcpyAsync(hs, status, size_t(nst) * 4, hipMemcpyDeviceToHost, h->stream));
         XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
+        if (nsum) XRS_HIP(hipMemcpyAsync(hd + 1024, nsum, d * 8, hipMemcpyDeviceToHost, h->stream));
         host_wait(h);
+        if (nsum)
+            for (size_t k = 0; k < d; ++k) ng[k] = size_t(hd[1024 + k] + 0.5);
         bool ok = true;
         for (int i = 0; i < nst; ++i) ok = ok && hs[i] == 0;
         worst = 0.0;
@@ -278,14 +301,20 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
     std::vector<int*> jst;   // Jacobi statuses
     for (size_t k = d - 1; k >= 1; --k) {
-        const size_t r = rr[k], N = t.n[k] * rr[k + 1];
-        const size_t kk = std::min({r, N, max_ranks[k - 1]});
-        const bool wide = r <= N;
+        const size_t r = rr[k], N = t.n[k] * rr[k + 1], Ng = ng[k] * rr[k + 1];   // local / global columns
+        const size_t kk = std::min({r, Ng, max_ranks[k - 1]});
+        const bool wide = r <= Ng;
+        if (!wide && t.sharded()) {   // the N x N Gram of a tall edge spans the ranks' column blocks
+            if (dbg) std::fprintf(stderr, "round_truncate: sharded tall edge %zu -> not certified\n", k);
+            sw.discard();
+            return false;
+        }
         const size_t g = wide ? r : N;
         double* B = A[k];
         double* P = sw.buf(g * g);
         if (wide) gemm_sym(h, P, g, 1.0, B, N, false, N, B, N, true);
         else gemm_sym(h, P, g, 1.0, B, N, true, r, B, N, false);
+        if (wide) t.reduce(P, g * g);   // sharded: sum over the mode slices
         double* L = sw.buf(g * g);
         double* Z = g > 256 ? sw.buf(g * g) : nullptr;   // (factor_big always builds L^{-1})
         const std::vector<CholJob> cj{{P, int(g), L, Z}, {P, int(g), nullptr, nullptr}};
@@ -327,7 +356,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         for (size_t k = 1; k < d; ++k) {
             X.push_back(A[k]);
             m.push_back(rr[k]);
-            n.push_back(t.n[k] * rr[k + 1]);
+            n.push_back(t.n[k] * rr[k + 1]);   // (local columns; the Grams are all-reduced)
         }
         orth_devs(sw, X, m, n, true, devb.d());
     }

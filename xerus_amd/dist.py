@@ -91,11 +91,59 @@ class TorchAllReduce:
                 return 1
 
         self.fn = ALLREDUCE_FN(_cb)   # keep a reference: the C side only holds the pointer
+        self.ctx = None
 
     @property
     def c_fn(self):
         # one rank: no hook at all (the C side then skips the stream synchronisation a hook needs)
         return None if self.single else C.cast(self.fn, C.c_void_p)
+
+
+class RcclComm:
+    """The library's own RCCL communicator (xrs_comm_t) as the all-reduce hook: collectives are enqueued
+    on the handle's stream by C++ (xrs_comm_allreduce), no Python callback and no host synchronisation per
+    collective. The 128-byte unique id is broadcast over the existing torch.distributed group."""
+
+    def __init__(self, handle: capi.Handle, group=None):
+        import torch.distributed as dist
+
+        self.handle, self.lib = handle, handle.lib
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        buf = C.create_string_buffer(128)
+        if rank == 0:
+            capi._check("xrs_comm_unique_id", self.lib.xrs_comm_unique_id(buf))
+        if world > 1:
+            obj = [bytes(buf.raw) if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0, group=group)
+            buf = C.create_string_buffer(obj[0], 128)
+        self.comm = C.c_void_p()
+        capi._check("xrs_comm_create", self.lib.xrs_comm_create(handle.h, world, rank, buf, C.byref(self.comm)))
+        self.world, self.rank = world, rank
+        self.device_native = True
+
+    @property
+    def c_fn(self):
+        return C.cast(self.lib.xrs_comm_allreduce, C.c_void_p)
+
+    @property
+    def ctx(self):
+        return self.comm
+
+    @property
+    def calls(self) -> int:
+        return int(self.lib.xrs_comm_calls(self.comm))
+
+    def close(self):
+        if self.comm:
+            capi._check("xrs_comm_destroy", self.lib.xrs_comm_destroy(self.comm))
+            self.comm = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class ShardedTT:
@@ -113,8 +161,9 @@ class ShardedTT:
     def ranks(self):
         return self.local.ranks
 
-    def round(self, max_ranks, comm: TorchAllReduce, eps: float = 8 * np.finfo(float).eps) -> bool:
-        """Certified sharded round in place; returns False (cores untouched) if the certificate fails."""
+    def round(self, max_ranks, comm, eps: float = 8 * np.finfo(float).eps) -> bool:
+        """Certified sharded round in place (TorchAllReduce or RcclComm); returns False (cores untouched) if
+        the certificate fails -- gather and round on one device then."""
         t = self.local
         d = t.order
         if isinstance(max_ranks, (int, np.integer)):
@@ -122,7 +171,7 @@ class ShardedTT:
         n, r, cores = t._arrays()
         mr = capi._arr(list(max_ranks) + [1])
         cert = C.c_int(0)
-        st = self.handle.lib.xrs_tt_round_sharded(self.handle.h, d, n, r, cores, mr, eps, comm.c_fn, None,
+        st = self.handle.lib.xrs_tt_round_sharded(self.handle.h, d, n, r, cores, mr, eps, comm.c_fn, comm.ctx,
                                                   C.byref(cert))
         t._writeback(r, cores)
         capi._check("xrs_tt_round_sharded", st)
@@ -130,7 +179,7 @@ class ShardedTT:
             t.canonicalized, t.core_position = True, 0
         return bool(cert.value)
 
-    def dot(self, other: "ShardedTT", comm: TorchAllReduce) -> float:
+    def dot(self, other: "ShardedTT", comm) -> float:
         x, y = self.local, other.local
         if self.dims != other.dims or x.dims != y.dims:
             raise ValueError(f"dot of sharded TTs with different dimensions: {self.dims} vs {other.dims}")
@@ -140,7 +189,7 @@ class ShardedTT:
         yc = (capi._DP * d)(*[capi._DP(p) for p in y.ptrs])
         capi._check("xrs_tt_dot_sharded",
                     self.handle.lib.xrs_tt_dot_sharded(self.handle.h, C.byref(out), d, capi._arr(x.dims),
-                                                       capi._arr(x.r), xc, capi._arr(y.r), yc, comm.c_fn, None))
+                                                       capi._arr(x.r), xc, capi._arr(y.r), yc, comm.c_fn, comm.ctx))
         return out.value
 
     def gather(self, all_gather_object: Callable) -> list[np.ndarray]:
