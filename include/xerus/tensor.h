@@ -192,8 +192,6 @@ std::ostream& operator<<(std::ostream& _out, const Tensor& _tensor);
 
 namespace misc {
 enum class FileFormat { BINARY, TSV };
-void save_to_file(const Tensor& _tensor, const std::string& _filename, const FileFormat _format = FileFormat::BINARY);
-Tensor load_tensor_from_file(const std::string& _filename);
 }  // namespace misc
 
 }  // namespace xerus

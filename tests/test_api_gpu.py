@@ -240,7 +240,53 @@ def test_save_load_roundtrip(xe, tmp_path):
         f = str(tmp_path / f"t{int(tsv)}.xrs")
         xe.save_to_file(A, f, tsv)
         B = xe.load_from_file(f)
-        np.testing.assert_array_equal(B.to_ndarray(), 2.5 * a)
+        if tsv:   # the reference writes digits10 + 1 = 16 significant digits (tensor.cpp:1783)
+            np.testing.assert_allclose(B.to_ndarray(), 2.5 * a, rtol=1e-15, atol=0)
+        else:
+            np.testing.assert_array_equal(B.to_ndarray(), 2.5 * a)
+    # byte layout of the binary stream (misc/fileIO.h:103-118, tensor.cpp:1781-1804)
+    from ttutil import read_xerus_file
+
+    kind, payload = read_xerus_file(str(tmp_path / "t0.xrs"))
+    assert kind == "xerus::Tensor"
+    assert payload["dims"] == [3, 4, 2]
+    np.testing.assert_array_equal(payload["data"].reshape(3, 4, 2), 2.5 * a)
+
+
+def test_tt_file_roundtrip_and_layout(xe, tmp_path):
+    """TTTensor files (ttNetwork.cpp:1455-1487 + tensorNetwork.cpp:1429-1466): the reference's node layout
+    (ghost ones({1}) nodes around the components), canonical flag and core position, both formats."""
+    from ttutil import read_xerus_file
+
+    xe.seed(7)
+    x = xe.TTTensor.random([4, 5, 3, 6], [3, 4, 5])
+    dense = xe.Tensor(x).to_ndarray()
+    for tsv in (False, True):
+        f = str(tmp_path / f"tt{int(tsv)}.xrs")
+        xe.save_to_file(x, f, tsv)
+        assert xe.file_type(f) == "xerus::TTNetwork<false>"
+        y = xe.load_from_file(f)
+        assert y.ranks() == x.ranks() and y.canonicalized == x.canonicalized and y.corePosition == x.corePosition
+        np.testing.assert_allclose(xe.Tensor(y).to_ndarray(), dense, rtol=0, atol=1e-14 * np.abs(dense).max())
+    kind, p = read_xerus_file(str(tmp_path / "tt0.xrs"))
+    assert kind == "xerus::TTNetwork<false>"
+    assert p["canonicalized"] is True and p["corePosition"] == 0
+    net = p["network"]
+    d = 4
+    assert net["dims"] == [4, 5, 3, 6]
+    assert net["external"] == [(k + 1, 1, n) for k, n in enumerate([4, 5, 3, 6])]
+    assert len(net["nodes"]) == d + 2
+    assert net["nodes"][0]["links"] == [(False, 1, 0, 1)]
+    assert net["nodes"][d + 1]["links"] == [(False, d, 2, 1)]
+    ranks = [1] + x.ranks() + [1]
+    for k in range(d):
+        links = net["nodes"][k + 1]["links"]
+        assert links[0] == (False, k, 0 if k == 0 else 2, ranks[k])
+        assert links[1] == (True, 2 ** 64 - 1, k, [4, 5, 3, 6][k])
+        assert links[2] == (False, k + 2, 0, ranks[k + 1])
+        np.testing.assert_array_equal(net["nodes"][k + 1]["tensor"]["data"],
+                                      x.get_component(k).to_ndarray().ravel())
+    assert net["nodes"][0]["tensor"]["dims"] == [1] and net["nodes"][0]["tensor"]["data"][0] == 1.0
 
 
 def test_factorisations(xe):

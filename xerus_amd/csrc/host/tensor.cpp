@@ -772,68 +772,5 @@ bool approx_entrywise_equal(const Tensor& _tensor, const std::vector<value_t>& _
     return true;
 }
 
-// ------------------------------------------------------------------------------------------------ file format
-// "Xerus Tensor datafile.\nFormat: Binary\n" + version, degree, dims, representation, data
-// (misc/fileIO.h:103-163, tensor.cpp:1781-1845; dense payload only)
-namespace misc {
-void save_to_file(const Tensor& _tensor, const std::string& _filename, const FileFormat _format) {
-    std::ofstream out(_filename, std::ios::binary);
-    XERUS_REQUIRE(out.good(), "cannot open " << _filename);
-    const auto v = _tensor.to_host();
-    if (_format == FileFormat::BINARY) {
-        out << "Xerus Tensor datafile.\nFormat: Binary\n";
-        const uint64 version = 1, degree = _tensor.degree(), rep = 1;
-        out.write(reinterpret_cast<const char*>(&version), 8);
-        out.write(reinterpret_cast<const char*>(&degree), 8);
-        for (size_t d : _tensor.dimensions) {
-            const uint64 dd = d;
-            out.write(reinterpret_cast<const char*>(&dd), 8);
-        }
-        out.write(reinterpret_cast<const char*>(&rep), 8);
-        out.write(reinterpret_cast<const char*>(v.data()), std::streamsize(v.size() * 8));
-    } else {
-        out << "Xerus Tensor datafile.\nFormat: TSV\n1\n" << _tensor.degree() << "\n";
-        for (size_t d : _tensor.dimensions) out << d << " ";
-        out << "\n1\n" << std::setprecision(17);
-        for (double x : v) out << x << "\n";
-    }
-}
-
-Tensor load_tensor_from_file(const std::string& _filename) {
-    std::ifstream in(_filename, std::ios::binary);
-    XERUS_REQUIRE(in.good(), "cannot open " << _filename);
-    std::string l1, l2;
-    std::getline(in, l1);
-    std::getline(in, l2);
-    XERUS_REQUIRE(l1 == "Xerus Tensor datafile.", "not a xerus Tensor file");
-    if (l2 == "Format: Binary") {
-        uint64 version, degree;
-        in.read(reinterpret_cast<char*>(&version), 8);
-        in.read(reinterpret_cast<char*>(&degree), 8);
-        Tensor::DimensionTuple dims(degree);
-        for (auto& d : dims) {
-            uint64 dd;
-            in.read(reinterpret_cast<char*>(&dd), 8);
-            d = dd;
-        }
-        uint64 rep;
-        in.read(reinterpret_cast<char*>(&rep), 8);
-        XERUS_REQUIRE(rep == 1, "only dense tensor files are supported");
-        size_t n = product(dims);
-        std::unique_ptr<value_t[]> data(new value_t[n]);
-        in.read(reinterpret_cast<char*>(data.get()), std::streamsize(n * 8));
-        return Tensor(dims, std::move(data));
-    }
-    size_t version, degree, rep;
-    in >> version >> degree;
-    Tensor::DimensionTuple dims(degree);
-    for (auto& d : dims) in >> d;
-    in >> rep;
-    size_t n = product(dims);
-    std::unique_ptr<value_t[]> data(new value_t[n]);
-    for (size_t i = 0; i < n; ++i) in >> data[i];
-    return Tensor(dims, std::move(data));
-}
-}  // namespace misc
 
 }  // namespace xerus

@@ -212,7 +212,18 @@ PYBIND11_MODULE(xerus, m) {
     m.def("save_to_file", [](const Tensor& _t, const std::string& _f, bool _tsv) {
         misc::save_to_file(_t, _f, _tsv ? misc::FileFormat::TSV : misc::FileFormat::BINARY);
     }, py::arg("tensor"), py::arg("filename"), py::arg("tsv") = false);
-    m.def("load_from_file", &misc::load_tensor_from_file);
+    m.def("save_to_file", [](const TTTensor& _t, const std::string& _f, bool _tsv) {
+        misc::save_to_file(_t, _f, _tsv ? misc::FileFormat::TSV : misc::FileFormat::BINARY);
+    }, py::arg("tt"), py::arg("filename"), py::arg("tsv") = false);
+    // the object type is read from the file's header (Tensor, TTTensor; a TensorNetwork file loads as its
+    // contracted Tensor)
+    m.def("load_from_file", [](const std::string& _f) -> py::object {
+        const std::string type = misc::file_type(_f);
+        if (type == "xerus::TTNetwork<false>") return py::cast(misc::load_tt_from_file(_f));
+        if (type == "xerus::TensorNetwork") return py::cast(misc::load_network_from_file(_f).to_tensor());
+        return py::cast(misc::load_tensor_from_file(_f));
+    });
+    m.def("file_type", &misc::file_type);
 
     // ------------------------------------------------------------------ TTTensor
     py::class_<IndexedTensor<TTTensor>>(m, "IndexedTTTensor")

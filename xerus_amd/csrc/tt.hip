@@ -772,6 +772,22 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     return true;
 }
 
+// One right chain pass (CholeskyQR on the whole train) over cores 1..d-1 that are already nearly
+// right-orthonormal -- the truncating round's output when its Gram-based cores missed the tolerance:
+// same tensor and ranks, orthonormality restored to ~u. False (cores untouched) if the pass failed.
+bool reorthonormalize(TT& t) {
+    int* hs = static_cast<int*>(t.h->host_scratch) + 12288;
+    ChainPass p;
+    chain_pass(t, false, p, hs);
+    const double dev = chain_check(t, p.C);
+    const bool ok = chain_status_ok(p) && dev <= kOrthTol;
+    for (size_t k = 0; k < t.d; ++k) {
+        if (ok) t.replace(k, p.C[k]);
+        else t.release(p.C[k]);
+    }
+    return ok;
+}
+
 // Sequential certified right-to-left CholeskyQR sweep from edge `from` down to 1 (the unfoldings are
 // already certified on the left with constant cX); an uncertified LQ hands over to the reference
 // algorithm at that edge.

@@ -89,6 +89,9 @@ void orth_right(TT& t, size_t k);
 size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps);
 void truncate_edge(TT& t, size_t k, size_t max_rank, double eps);
 
+// one right chain pass restoring right-orthonormality of nearly orthonormal cores (tt.hip)
+bool reorthonormalize(TT& t);
+
 // certified truncating round (tt_trunc.hip): left-canonical chain pass + device-resident right-to-left
 // truncation sweep with one host synchronisation; false (cores untouched) when a certificate fails
 bool round_truncate(TT& t, const size_t* max_ranks, double eps);

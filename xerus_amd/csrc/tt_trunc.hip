@@ -33,7 +33,8 @@ namespace ttd {
 
 namespace {
 
-constexpr double kTruncOrthTol = 1e-12;   // max |C C^T - I| accepted for the new cores
+constexpr double kTruncOrthTol = 1e-12;    // max |C C^T - I| of a canonical core; above it: one chain pass
+constexpr double kTruncAcceptTol = 1e-8;   // above it the sweep is rejected (reference algorithm instead)
 
 // Host-side record of everything enqueued; buffers are released once the sweep is judged.
 struct Sweep {
@@ -376,13 +377,19 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     for (int i = 0; i < nchk2; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
     if (dbg) std::fprintf(stderr, "round_truncate: sweep %s, max Jacobi sweeps %d, orthogonality %.3e\n",
                           ok ? "certified" : "NOT certified", max_sweeps, worst);
-    if (!ok || !(worst <= kTruncOrthTol)) {
+    if (!ok || !(worst <= kTruncAcceptTol)) {
         sw.discard();
         return false;
     }
     for (size_t k = 0; k < d; ++k) t.replace(k, A[k]);
     sw.owned.clear();
     for (size_t k = 1; k < d; ++k) t.r[k] = rr[k];
+    // the new cores S^-1 U^T B carry kappa(B_kk)^2 u of non-orthogonality: one chain pass if that is
+    // above the canonical-form tolerance (the represented tensor and the ranks are final already)
+    if (worst > kTruncOrthTol) {
+        const bool re = reorthonormalize(t);
+        if (dbg) std::fprintf(stderr, "round_truncate: re-orthonormalised (%s)\n", re ? "ok" : "failed");
+    }
     return true;
 }
 
