@@ -126,6 +126,12 @@ int xrs_rq(xrs_handle_t handle, double* R, double* Q, const double* A, size_t m,
 /** Thin SVD A = U*diag(S)*Vt, U: m x k, S: k, Vt: k x n, k = min(m,n), S descending
  *  (replaces blasWrapper::svd / dgesdd 'S', blasLapackWrapper.cpp:201-232). */
 int xrs_svd(xrs_handle_t handle, double* U, double* S, double* Vt, const double* A, size_t m, size_t n);
+/** Singular values and right singular vectors of the rows of A (p x q, p <= q <= 512) by one-sided
+ *  Jacobi -- the SVD step of the truncating TT round (TTNetwork::round's per-edge svd,
+ *  ttNetwork.cpp:644-665, without U). S: p descending; Vt: p x q, orthonormal rows for S > 0.
+ *  kernel: 0 auto, 1 one workgroup, 2 multi-workgroup blocks (p > 16). *sweeps (host): Jacobi
+ *  sweeps used, -1 not converged, -2 grid-barrier timeout. Synchronises. */
+int xrs_svd_rows_vt(xrs_handle_t handle, double* S, double* Vt, int* sweeps, const double* A, size_t p, size_t q, int kernel);
 
 /* ---------------------------------------------------------------- TT hot path (ttNetwork.cpp) */
 /* A TT of order d is passed as d device core pointers; core k has dims (r[k], n[k], r[k+1]),

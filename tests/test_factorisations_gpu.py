@@ -110,3 +110,37 @@ def test_qr_graded_columns(handle, m, n, scale):
     Qh, Rh = Q.numpy(), R.numpy()
     assert _rel(Qh @ Rh, A) <= 1e-12
     assert np.linalg.norm(Qh.T @ Qh - np.eye(n)) <= TOL * n
+
+
+@pytest.mark.parametrize("p,q", [(17, 40), (100, 100), (128, 128), (129, 129), (200, 256), (256, 256), (300, 400),
+                                 (512, 512), (250, 500)])
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_svd_rows_vt_kernels(handle, p, q, kernel):
+    """The truncating round's Jacobi SVD (one workgroup vs the multi-workgroup block kernel) against LAPACK:
+    singular values to ~u*S0, orthonormal Vt, A Vt^T Vt = A. Graded spectrum as in a TT edge."""
+    rng = np.random.default_rng(p * 7 + q)
+    U0, _ = np.linalg.qr(rng.standard_normal((p, p)))
+    V0, _ = np.linalg.qr(rng.standard_normal((q, p)))
+    s0 = np.logspace(0, -9, p)
+    A = (U0 * s0) @ V0.T
+    S, Vt, sweeps = handle.svd_rows_vt(handle.array(A), kernel)
+    S, Vt = S.numpy(), Vt.numpy()
+    assert 0 < sweeps <= 40
+    assert np.all(np.diff(S) <= 0)
+    assert np.max(np.abs(S - s0)) <= 1e-14 * s0[0] * np.sqrt(p)
+    assert np.linalg.norm(Vt @ Vt.T - np.eye(p)) <= 1e-13 * p
+    assert _rel((A @ Vt.T) @ Vt, A) <= 1e-14 * np.sqrt(p)
+
+
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_svd_rows_vt_rank_deficient(handle, kernel):
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((200, 7)) @ rng.standard_normal((7, 300))
+    S, Vt, sweeps = handle.svd_rows_vt(handle.array(A), kernel)
+    S = S.numpy()
+    ref = np.linalg.svd(A, compute_uv=False)
+    assert sweeps > 0
+    assert np.max(np.abs(S[:7] - ref[:7])) <= 1e-13 * ref[0]
+    assert np.max(np.abs(S[7:])) <= 1e-12 * ref[0]
+    Vt7 = Vt.numpy()[:7]
+    assert np.linalg.norm(Vt7 @ Vt7.T - np.eye(7)) <= 1e-13

@@ -50,6 +50,7 @@ SIGNATURES = {
     "xrs_qr": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
     "xrs_rq": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
     "xrs_svd": (C.c_int, [_DP, _DP, _DP, _DP, _DP, _SZ, _SZ]),
+    "xrs_svd_rows_vt": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ, C.c_int]),
     "xrs_tt_move_core": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ, _SZ, C.c_int]),
     "xrs_tt_round": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ,
                                C.POINTER(_SZ), C.c_double]),
@@ -261,6 +262,13 @@ class Handle:
         U, S, Vt = self.empty((m, k)), self.empty((k,)), self.empty((k, n))
         _check("xrs_svd", self.lib.xrs_svd(self.h, _DP(U.ptr), _DP(S.ptr), _DP(Vt.ptr), _DP(A.ptr), m, n))
         return U, S, Vt
+
+    def svd_rows_vt(self, A: "DeviceArray", kernel: int = 0):
+        """(S, Vt, sweeps) of the rows of A (p <= q <= 512) by one-sided Jacobi (xrs_svd_rows_vt)."""
+        p, q = A.shape
+        S, Vt, sw = self.empty((p,)), self.empty((p, q)), C.c_int()
+        _check("xrs_svd_rows_vt", self.lib.xrs_svd_rows_vt(self.h, _DP(S.ptr), _DP(Vt.ptr), C.byref(sw), _DP(A.ptr), p, q, kernel))
+        return S, Vt, sw.value
 
     def last_round_path(self) -> str | None:
         """"chain" / "truncate" / "reference": the algorithm of this handle's last TT round."""

@@ -65,7 +65,9 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
     // former (k>>1) swizzle paired them: SQ_LDS_BANK_CONFLICT ~1 cycle per LDS instruction).
     constexpr int SA = BM;
     constexpr int SB = BN;
-    static_assert(BM % 32 == 0 && BN % 32 == 0, "swizzle needs 32-aligned tile rows");
+    static_assert(BM % 16 == 0 && BN % 16 == 0, "tile rows must be whole MFMA tiles");
+    // 32-aligned rows take the 32-wide swizzle; 16-aligned ones (80-wide tiles) stay inside their 16-group
+    constexpr bool WIDE_SWZ_A = BM % 32 == 0, WIDE_SWZ_B = BN % 32 == 0;
     constexpr int WM = BM / WGM, WN = BN / WGN;
     constexpr int TM = WM / 16, TN = WN / 16;
     static_assert(TM >= 1 && TN >= 1, "wave tile smaller than one MFMA tile");
@@ -123,7 +125,8 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j) acc2[a][i][j] = d4{0.0, 0.0, 0.0, 0.0};
-    auto swz = [](int k) { return ((k & 1) << 4) | (k & 15); };
+    auto swza = [](int k) { return WIDE_SWZ_A ? (((k & 1) << 4) | (k & 15)) : (k & 15); };
+    auto swzb = [](int k) { return WIDE_SWZ_B ? (((k & 1) << 4) | (k & 15)) : (k & 15); };
 
     // register ring: the global loads of K-step t+PD are issued while step t computes, so PD steps of
     // MFMA work cover the global-memory latency (one step is only ~4-8 MFMAs per wave)
@@ -166,14 +169,14 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
             const bool ok = (m0 + m < M) && (k0 + k < kend);
             // (no guard when the tile divides evenly over the threads: a branch here makes the waitcnt
             // pass lose track of the ring's loads and drain vmcnt(0) at the loop head)
-            if ((BM * GBK) % NT == 0 || tid + e * NT < BM * GBK) As[buf][k * SA + (m ^ swz(k))] = ok ? ra[slot][e] : 0.0;
+            if ((BM * GBK) % NT == 0 || tid + e * NT < BM * GBK) As[buf][k * SA + (m ^ swza(k))] = ok ? ra[slot][e] : 0.0;
         }
 #pragma unroll
         for (int e = 0; e < B_PER; ++e) {
             int n, k;
             b_coord(e, n, k);
             const bool ok = (n0 + n < N) && (k0 + k < kend);
-            if ((BN * GBK) % NT == 0 || tid + e * NT < BN * GBK) Bs[buf][k * SB + (n ^ swz(k))] = ok ? rb[slot][e] : 0.0;
+            if ((BN * GBK) % NT == 0 || tid + e * NT < BN * GBK) Bs[buf][k * SB + (n ^ swzb(k))] = ok ? rb[slot][e] : 0.0;
         }
     };
     const int lr = lane & 15, lk = lane >> 4;
@@ -185,9 +188,9 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
             const int kk = (q * WGK + kg) * 4;
             double af[TM], bf[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = as[(kk + lk) * SA + ((wm + i * 16 + lr) ^ swz(kk + lk))];
+            for (int i = 0; i < TM; ++i) af[i] = as[(kk + lk) * SA + ((wm + i * 16 + lr) ^ swza(kk + lk))];
 #pragma unroll
-            for (int j = 0; j < TN; ++j) bf[j] = bs[(kk + lk) * SB + ((wn + j * 16 + lr) ^ swz(kk + lk))];
+            for (int j = 0; j < TN; ++j) bf[j] = bs[(kk + lk) * SB + ((wn + j * 16 + lr) ^ swzb(kk + lk))];
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -411,8 +414,10 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     }
     // (batched: the tile counts are over the whole batch)
     auto ntiles = [&](int bm, int bn) { return long(count) * ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
-    const int bms[14] = {0, 128, 64, 64, 32, 64, 64, 64, 64, 32, 32, 32, 32, 64},
-              bns[14] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32, 32, 32, 32, 32};
+    //   v14 64x80 / v15 80x64 (8 waves, K split 2, K-step 32): 256 x 5120 and 5120 x 256 TT shapes in
+    //   exactly 256 tiles (one per CU)
+    const int bms[16] = {0, 128, 64, 64, 32, 64, 64, 64, 64, 32, 32, 32, 32, 64, 64, 80},
+              bns[16] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32, 32, 32, 32, 32, 80, 64};
     int var = cfg_var;
     long cfg_target_eff = cfg_target;
     static const long sym_target = [] {
@@ -473,11 +478,11 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         const long maxs = std::max<long>(1, K / cfg_kmin);
         splits = int(std::max<long>(1, std::min(want, maxs)));
     }
-    const int bk = ((var >= 5 && var <= 7) || var == 10 || var == 12 || var == 13) ? 32 : 16;
+    const int bk = ((var >= 5 && var <= 7) || var == 10 || var == 12 || var == 13 || var == 14 || var == 15) ? 32 : 16;
     int kps = (K + splits - 1) / splits;
     kps = (kps + bk - 1) / bk * bk;
     splits = (K + kps - 1) / kps;
-    if (std::is_same<PTR, GemmMany>::value && var >= 5) var = (var == 5 || var == 8 || var == 13) ? 3 : ((var == 9 || var >= 10) ? 4 : 2);   // tuning-only tiles: single GEMMs
+    if (std::is_same<PTR, GemmMany>::value && var >= 5 && var <= 13) var = (var == 5 || var == 8 || var == 13) ? 3 : ((var == 9 || var >= 10) ? 4 : 2);   // tuning-only tiles: single GEMMs
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
     // one-launch split-K when the tile grid fits the stream's ticket array (XRS_GEMM_SPLITK2=1: old
@@ -506,6 +511,8 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         case 11: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 16, 2, 2, 1, 2); break;
         case 12: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(32, 32, 32, 2, 2, 4, 2); break;
         case 13: if constexpr (std::is_same<PTR, GemmOne>::value) XRS_TILES(64, 32, 32, 2, 2, 2, 2); break;
+        case 14: XRS_TILES(64, 80, 32, 4, 1, 2, 2); break;
+        case 15: XRS_TILES(80, 64, 32, 1, 4, 2, 2); break;
         default: XRS_TILES(32, 32, 16, 2, 2, 2, 2); break;
     }
 #undef XRS_TILES

@@ -12,6 +12,8 @@
 // single-workgroup dgeqp3 emulation applied to the small n x n triangular factor, with the sign of
 // dgeqp3's R_00 taken from A itself (it is -sign(A[0][p]) for the first max-norm column p).
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "smallla.hpp"
 
@@ -379,6 +381,22 @@ int xrs_svd(xrs_handle_t h, double* U, double* S, double* Vt, const double* A, s
     return guarded([&] {
         XRS_REQUIRE(h && U && S && Vt && A, "null argument");
         svd(h, A, m, n, U, S, Vt);
+    });
+}
+
+int xrs_svd_rows_vt(xrs_handle_t h, double* S, double* Vt, int* sweeps, const double* A, size_t p, size_t q, int kernel) {
+    return guarded([&] {
+        XRS_REQUIRE(h && S && Vt && A && sweeps, "null argument");
+        XRS_REQUIRE(p >= 1 && p <= q && q <= 512, "xrs_svd_rows_vt: need 1 <= p <= q <= 512");
+        DevBuf st(h, 64);
+        XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
+        jacobi_vt(h, A, int(q), false, int(p), int(q), S, Vt, int(q), st.as<int>(), 40, kernel);
+        int sts[4];
+        read_status(h, st.as<int>(), 4, sts);
+        *sweeps = sts[0];
+        if (std::getenv("XRS_SVD_TIMING"))
+            std::fprintf(stderr, "jacobi_vt p=%zu q=%zu kernel=%d: sweeps %d, ticks total %d barrier %d exchange %d\n", p, q, kernel,
+                         sts[0], sts[1], sts[2], sts[3]);
     });
 }
 

@@ -16,6 +16,7 @@
 // nearly-identity rotations). 64 groups: up to 64 pairs per round in flight, one barrier per round.
 // Convergence: no pair with |w_i . w_j| > tol ||w_i|| ||w_j||, tol = sqrt(q) u (dgesvj's criterion).
 #include <cmath>
+#include <cstdlib>
 
 #include "smallla.hpp"
 
@@ -86,6 +87,88 @@ __device__ __forceinline__ void rotation(double a, double b, double c, double& s
     tau = s * frcp(1.0 + cs);   // Rutishauser: x' = x - s (y + tau x), y' = y + s (x - tau y)
 }
 
+// One Jacobi step on the row pair (wi, wj) of length q by a group of G lanes (lane l): orthogonalise the
+// rows if |wi . wj| > tol ||wi|| ||wj||; true if rotated. E > 0: q <= E * G, the lane's elements are held
+// in registers (all loads issued before any use); E = 0: any q, streamed.
+// The register core: the lane's E elements of each row (zero beyond q, which rotations keep zero)
+template <int G, int E>
+__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2) {
+    double a = 0.0, b = 0.0, c = 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        a = fma(x[e], x[e], a);
+        b = fma(y[e], y[e], b);
+        c = fma(x[e], y[e], c);
+    }
+    a = gsum<G>(a);
+    b = gsum<G>(b);
+    c = gsum<G>(c);
+    if (!(c * c > tol2 * a * b)) return false;
+    double s, tau;
+    rotation(a, b, c, s, tau);
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const double xe = x[e], ye = y[e];
+        x[e] = xe - s * fma(tau, xe, ye);
+        y[e] = ye + s * fma(-tau, ye, xe);
+    }
+    return true;
+}
+
+template <int G, int E>
+__device__ __forceinline__ void load_row(double (&x)[E], const double* __restrict__ w, int q, int l) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int k = l + e * G;
+        x[e] = k < q ? w[k] : 0.0;
+    }
+}
+
+template <int G, int E>
+__device__ __forceinline__ void store_row(const double (&x)[E], double* __restrict__ w, int q, int l) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int k = l + e * G;
+        if (k < q) w[k] = x[e];
+    }
+}
+
+// One Jacobi step on the row pair (wi, wj) of length q by a group of G lanes (lane l): orthogonalise the
+// rows if |wi . wj| > tol ||wi|| ||wj||; true if rotated. E > 0: q <= E * G, the lane's elements are held
+// in registers (all loads issued before any use); E = 0: any q, streamed.
+template <int G, int E>
+__device__ __forceinline__ bool rotate_pair(double* __restrict__ wi, double* __restrict__ wj, int q, int l, double tol2) {
+    if constexpr (E > 0) {
+        double x[E], y[E];
+        load_row<G, E>(x, wi, q, l);
+        load_row<G, E>(y, wj, q, l);
+        if (!rotate_regs<G, E>(x, y, tol2)) return false;
+        store_row<G, E>(x, wi, q, l);
+        store_row<G, E>(y, wj, q, l);
+        return true;
+    } else {
+        double a = 0.0, b = 0.0, c = 0.0;
+        for (int k = l; k < q; k += G) {
+            const double x = wi[k], y = wj[k];
+            a = fma(x, x, a);
+            b = fma(y, y, b);
+            c = fma(x, y, c);
+        }
+        a = gsum<G>(a);
+        b = gsum<G>(b);
+        c = gsum<G>(c);
+        if (!(c * c > tol2 * a * b)) return false;
+        double s, tau;
+        rotation(a, b, c, s, tau);
+        for (int k = l; k < q; k += G) {
+            const double x = wi[k], y = wj[k];
+            wi[k] = x - s * fma(tau, x, y);
+            wj[k] = y + s * fma(-tau, y, x);
+        }
+        return true;
+    }
+}
+
 // player at position x of round `round` (circle method, P players, position 0 fixed)
 __device__ __forceinline__ int player(int x, int round, int P) { return x == 0 ? 0 : 1 + (x - 1 + round) % (P - 1); }
 
@@ -130,62 +213,7 @@ __device__ void jacobi_rows_body(double* __restrict__ W, int ldw, const double* 
                 j = P - 1 - t + round;
                 j = j >= P ? j - (P - 1) : j;
                 if (i >= p || j >= p) continue;
-                double* wi = W + size_t(i) * ldw;
-                double* wj = W + size_t(j) * ldw;
-                if constexpr (E > 0) {
-                    // the lane's E elements of both rows in registers: all loads issued before any use
-                    double x[E], y[E];
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        const int k = l + e * G;
-                        x[e] = k < q ? wi[k] : 0.0;
-                        y[e] = k < q ? wj[k] : 0.0;
-                    }
-                    double a = 0.0, b = 0.0, c = 0.0;
-#pragma unroll
-                    for (int e = 0; e < E; ++e) {
-                        a = fma(x[e], x[e], a);
-                        b = fma(y[e], y[e], b);
-                        c = fma(x[e], y[e], c);
-                    }
-                    a = gsum<G>(a);
-                    b = gsum<G>(b);
-                    c = gsum<G>(c);
-                    if (c * c > tol2 * a * b) {
-                        double s, tau;
-                        rotation(a, b, c, s, tau);
-#pragma unroll
-                        for (int e = 0; e < E; ++e) {
-                            const int k = l + e * G;
-                            if (k < q) {
-                                wi[k] = x[e] - s * fma(tau, x[e], y[e]);
-                                wj[k] = y[e] + s * fma(-tau, y[e], x[e]);
-                            }
-                        }
-                        if (l == 0) rotated = 1;
-                    }
-                } else {
-                    double a = 0.0, b = 0.0, c = 0.0;
-                    for (int k = l; k < q; k += G) {
-                        const double x = wi[k], y = wj[k];
-                        a = fma(x, x, a);
-                        b = fma(y, y, b);
-                        c = fma(x, y, c);
-                    }
-                    a = gsum<G>(a);
-                    b = gsum<G>(b);
-                    c = gsum<G>(c);
-                    if (c * c > tol2 * a * b) {
-                        double s, tau;
-                        rotation(a, b, c, s, tau);
-                        for (int k = l; k < q; k += G) {
-                            const double x = wi[k], y = wj[k];
-                            wi[k] = x - s * fma(tau, x, y);
-                            wj[k] = y + s * fma(-tau, y, x);
-                        }
-                        if (l == 0) rotated = 1;
-                    }
-                }
+                if (rotate_pair<G, E>(W + size_t(i) * ldw, W + size_t(j) * ldw, q, l, tol2) && l == 0) rotated = 1;
             }
             __syncthreads();
         }
@@ -236,22 +264,220 @@ __global__ void __launch_bounds__(SVG_THREADS) k_jacobi_vt_global(double* __rest
     else jacobi_rows_body<16, SVG_THREADS, 0>(Wg, q, Win, ldin, trans != 0, p, q, max_sweeps, S, Vt, ldvt, status);
 }
 
+
+// ---- multi-workgroup block Jacobi (p > 128): the rows are cut into nb blocks of SVB_ROWS (the last ones
+// padded with zero rows); workgroup w holds the block pair at positions (w, nb-1-w) of the circle
+// tournament over blocks -- 2 SVB_ROWS rows x q in LDS -- and orthogonalises its rows with one inner
+// sweep (2 SVB_ROWS - 1 rounds of SVB_ROWS disjoint pairs, a 16-lane group per pair); then every block
+// goes through global memory to the workgroup that pairs it next (one grid barrier per outer round).
+// nb - 1 outer rounds are one sweep; converged when a whole sweep rotated nothing.
+// Grid barrier: monotone counter; producer = every wave's vmcnt(0) + barrier + lane-0 agent release
+// fence, consumer = relaxed poll + agent acquire fence (MI355X_MICROARCH.md, inter-workgroup
+// visibility). The poll is bounded (status -2 instead of a hang if a workgroup were never scheduled).
+constexpr int SVB_ROWS = 16, SVB_G = 16, SVB_THREADS = SVB_ROWS * SVB_G, SVB_QMAX = 512;
+constexpr int SVB_SYNC_WORDS = 64;   // [0] barrier counter, [1 + sweep] rotated flags
+
+__device__ __forceinline__ void grid_barrier(unsigned* counter, unsigned target, int* err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 26)) {
+                *err = 1;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+template <int E>
+__global__ void __launch_bounds__(SVB_THREADS) k_jacobi_vt_blocks(const double* __restrict__ Win, int ldin, int trans, int p, int q,
+                                                                  int nb, int max_sweeps, double* __restrict__ slots,
+                                                                  unsigned* __restrict__ sync, double* __restrict__ norms,
+                                                                  double* __restrict__ S, double* __restrict__ Vt, int ldvt,
+                                                                  int* __restrict__ status) {
+    constexpr int R2 = 2 * SVB_ROWS;
+    __shared__ double Ws[R2 * (SVB_QMAX + 1)];
+    __shared__ int rotated, err;
+    __shared__ int part[SVB_THREADS / 64];
+    const int tid = threadIdx.x, g = tid / SVB_G, l = tid % SVB_G;
+    const int w = blockIdx.x, nwg = gridDim.x;
+    const int ldw = q + ((q & 1) ? 0 : 1);
+    const double tol = sqrt(double(q)) * 1.1102230246251565e-16;
+    const double tol2 = tol * tol;
+    if (tid == 0) err = 0;
+    // block id at tournament position x in outer round t
+    auto block_at = [&](int x, int t) { return x == 0 ? 0 : 1 + (x - 1 + t) % (nb - 1); };
+    auto row_of = [&](int r, int top, int bot) { return (r < SVB_ROWS ? top : bot) * SVB_ROWS + (r % SVB_ROWS); };
+    auto load_blocks = [&](int top, int bot, bool from_input) {
+        for (int e = tid; e < R2 * q; e += SVB_THREADS) {
+            const int r = e / q, k = e - r * q;
+            const int row = row_of(r, top, bot);
+            double v = 0.0;
+            if (row < p) {
+                if (from_input) v = trans ? Win[size_t(k) * ldin + row] : Win[size_t(row) * ldin + k];
+                else v = slots[size_t(row) * q + k];
+            }
+            Ws[r * ldw + k] = v;
+        }
+    };
+    auto store_blocks = [&](int top, int bot) {
+        for (int e = tid; e < R2 * q; e += SVB_THREADS) {
+            const int r = e / q, k = e - r * q;
+            slots[size_t(row_of(r, top, bot)) * q + k] = Ws[r * ldw + k];
+        }
+    };
+    unsigned barriers = 0;
+    long long t_bar = 0, t_xch = 0;
+    const long long t_start = wall_clock64();
+    int top = block_at(w, 0), bot = block_at(nb - 1 - w, 0);
+    load_blocks(top, bot, true);
+    __syncthreads();
+    int sweep = 0;
+    bool converged = false;
+    while (sweep < max_sweeps && !converged) {
+        if (tid == 0) rotated = 0;
+        __syncthreads();
+        for (int t = 0; t < nb - 1; ++t) {
+            if (t == 0) {
+                // first outer round of the sweep: the pairs inside each block (circle method over
+                // SVB_ROWS rows; groups 0..7 on the top block, 8..15 on the bottom one)
+                constexpr int HALF = SVB_ROWS / 2;
+                const int gg = g % HALF, base = g < HALF ? 0 : SVB_ROWS;
+                for (int round = 0; round < SVB_ROWS - 1; ++round) {
+                    const int i = player(gg, round, SVB_ROWS), j = player(SVB_ROWS - 1 - gg, round, SVB_ROWS);
+                    if (rotate_pair<SVB_G, E>(Ws + (base + i) * ldw, Ws + (base + j) * ldw, q, l, tol2) && l == 0) rotated = 1;
+                    __syncthreads();
+                }
+            }
+            // the pairs across the two blocks: group g keeps top row g in registers and meets bottom row
+            // (g + s) mod SVB_ROWS in round s
+            {
+                double x[E], y[E];
+                load_row<SVB_G, E>(x, Ws + g * ldw, q, l);
+                bool rot = false;
+                for (int sr = 0; sr < SVB_ROWS; ++sr) {
+                    double* wb = Ws + (SVB_ROWS + ((g + sr) & (SVB_ROWS - 1))) * ldw;
+                    load_row<SVB_G, E>(y, wb, q, l);
+                    if (rotate_regs<SVB_G, E>(x, y, tol2)) {
+                        rot = true;
+                        store_row<SVB_G, E>(y, wb, q, l);
+                    }
+                    __syncthreads();
+                }
+                store_row<SVB_G, E>(x, Ws + g * ldw, q, l);
+                if (rot && l == 0) rotated = 1;
+                __syncthreads();
+            }
+            // exchange: every block to the slot of its id, then the pair of the next outer round
+            const long long t0 = wall_clock64();
+            store_blocks(top, bot);
+            if (t == nb - 2 && tid == 0 && rotated)
+                __hip_atomic_fetch_or(&sync[1 + sweep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const long long t1 = wall_clock64();
+            grid_barrier(&sync[0], ++barriers * unsigned(nwg), &err);
+            const long long t2 = wall_clock64();
+            const int tn = (t + 1) % (nb - 1);
+            top = block_at(w, tn);
+            bot = block_at(nb - 1 - w, tn);
+            load_blocks(top, bot, false);
+            __syncthreads();
+            t_bar += t2 - t1;
+            t_xch += (t1 - t0) + (wall_clock64() - t2);
+        }
+        // every workgroup reads the same flag (all were set before the last barrier of the sweep)
+        if (tid == 0) rotated = int(__hip_atomic_load(&sync[1 + sweep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        __syncthreads();
+        converged = rotated == 0;
+        ++sweep;
+        if (err) break;
+        __syncthreads();
+    }
+    // singular values = row norms; global ranks after one more barrier
+    for (int r = g; r < R2; r += SVB_ROWS) {
+        const double* wr = Ws + r * ldw;
+        double a = 0.0;
+        for (int k = l; k < q; k += SVB_G) a = fma(wr[k], wr[k], a);
+        a = gsum<SVB_G>(a);
+        const int row = row_of(r, top, bot);
+        if (l == 0 && row < p) norms[row] = sqrt(a);
+    }
+    grid_barrier(&sync[0], ++barriers * unsigned(nwg), &err);
+    for (int r = 0; r < R2; ++r) {
+        const int row = row_of(r, top, bot);
+        if (row >= p) continue;
+        const double si = norms[row];
+        int rk = 0;
+        for (int j2 = tid; j2 < p; j2 += SVB_THREADS) {
+            const double sj = norms[j2];
+            rk += (sj > si) || (sj == si && j2 < row);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) rk += __shfl_xor(rk, o, 64);
+        if ((tid & 63) == 0) part[tid >> 6] = rk;
+        __syncthreads();
+        int rank = 0;
+#pragma unroll
+        for (int i = 0; i < SVB_THREADS / 64; ++i) rank += part[i];
+        __syncthreads();
+        if (tid == 0) S[rank] = si;
+        const double inv = si > 0.0 ? 1.0 / si : 0.0;
+        for (int k = tid; k < q; k += SVB_THREADS) Vt[size_t(rank) * ldvt + k] = Ws[r * ldw + k] * inv;
+    }
+    if (w == 0 && tid == 0) {
+        status[0] = err ? -2 : (converged ? sweep : -1);
+        status[1] = int(wall_clock64() - t_start);   // 100 MHz ticks (diagnostics)
+        status[2] = int(t_bar);
+        status[3] = int(t_xch);
+    }
+}
+
 }  // namespace
 
 bool jacobi_vt_fits_lds(int p, int q) { return q <= 128 && size_t(p) * size_t(q + 1) <= size_t(SV_LDS); }
 
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
-               int* status_dev, int max_sweeps) {
+               int* status_dev, int max_sweeps, int kernel) {
     XRS_REQUIRE(p >= 1 && p <= SV_MAXP && p <= q, "jacobi_vt: need 1 <= p <= min(q, 512)");
+    XRS_REQUIRE(kernel >= 0 && kernel <= 2, "jacobi_vt: kernel is 0 (auto), 1 (one workgroup) or 2 (blocks)");
     KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * q * 6.0, 16.0 * double(p) * q);
-    if (jacobi_vt_fits_lds(p, q)) {
+    // smallest p handed to the multi-workgroup block kernel (XRS_SVD_BLOCK_MIN tunes it)
+    static const int block_min = [] {
+        const char* e = std::getenv("XRS_SVD_BLOCK_MIN");
+        return e ? std::atoi(e) : 129;
+    }();
+    const bool blocks_ok = p > SVB_ROWS && q <= SVB_QMAX;
+    XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs 16 < p and q <= 512");
+    if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
+        int nb = (p + SVB_ROWS - 1) / SVB_ROWS;
+        nb += nb & 1;
+        const int sweeps = std::min(max_sweeps, SVB_SYNC_WORDS - 1);
+        DevBuf slots(h, size_t(nb) * SVB_ROWS * q * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
+        XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
+        // nb / 2 <= 16 one-CU workgroups: co-resident on any MI355X (the barrier needs all of them live)
+        if (q <= 256)
+            hipLaunchKernelGGL(k_jacobi_vt_blocks<16>, dim3(nb / 2), dim3(SVB_THREADS), 0, h->stream, W, ldw, int(trans), p, q, nb,
+                               sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
+        else
+            hipLaunchKernelGGL(k_jacobi_vt_blocks<32>, dim3(nb / 2), dim3(SVB_THREADS), 0, h->stream, W, ldw, int(trans), p, q, nb,
+                               sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
+        check_launch("k_jacobi_vt_blocks");
+    } else if (jacobi_vt_fits_lds(p, q)) {
         hipLaunchKernelGGL(k_jacobi_vt_lds, dim3(1), dim3(SVL_THREADS), 0, h->stream, W, ldw, int(trans), p, q, max_sweeps, S, Vt,
                            ldvt, status_dev);
         check_launch("k_jacobi_vt_lds");
     } else {
         DevBuf Wg(h, size_t(p) * q * 8);
-        hipLaunchKernelGGL(k_jacobi_vt_global, dim3(1), dim3(SVG_THREADS), 0, h->stream, Wg.d(), W, ldw, int(trans), p, q, max_sweeps, S,
-                           Vt, ldvt, status_dev);
+        hipLaunchKernelGGL(k_jacobi_vt_global, dim3(1), dim3(SVG_THREADS), 0, h->stream, Wg.d(), W, ldw, int(trans), p, q, max_sweeps,
+                           S, Vt, ldvt, status_dev);
         check_launch("k_jacobi_vt_global");
     }
 }
