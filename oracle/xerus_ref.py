@@ -351,6 +351,26 @@ class TT:
         return float(np.sqrt(max(0.0, dot(self, self))))
 
 
+def tt_svd(full: np.ndarray, eps: float, max_ranks: Sequence[int]) -> TT:
+    """TT-SVD constructor TTNetwork(const Tensor&, eps, maxRanks) (ttNetwork.cpp:112-160): right to left,
+    calculate_svd(remains, S, node, remains, 1 + position, maxRanks[position - 1], eps) with the cut of
+    tensor.cpp:1462-1474, node -> component `position`, remains <- U S; the rest is component 0, core at 0."""
+    dims = tuple(full.shape)
+    d = len(dims)
+    assert len(max_ranks) == d - 1
+    remains = np.asarray(full, dtype=np.float64).reshape((1,) + dims + (1,))
+    cores: List[np.ndarray] = [None] * d  # type: ignore[list-item]
+    for pos in range(d - 1, 0, -1):
+        split = 1 + pos
+        sh = remains.shape
+        u, s, vt = svd(remains.reshape(int(np.prod(sh[:split])), -1))
+        r = svd_rank(s, max_ranks[pos - 1], eps)
+        cores[pos] = np.ascontiguousarray(vt[:r].reshape((r,) + sh[split:]))
+        remains = (u[:, :r] * s[:r]).reshape(sh[:split] + (r,))
+    cores[0] = np.ascontiguousarray(remains)
+    return TT(cores, True, 0)
+
+
 def dot(x: TT, y: TT) -> float:
     """<x,y> as a left-to-right zipper (the order the reference's heuristics pick)."""
     E = np.ones((1, 1))

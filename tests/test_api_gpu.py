@@ -382,3 +382,24 @@ def test_tt_round_truncates_like_oracle(xe, ref):
     assert x.ranks() == ox.ranks
     err_gpu = np.linalg.norm(xe.Tensor(x).to_ndarray() - ox.full())
     assert err_gpu <= 1e-8 * np.linalg.norm(ox.full())
+
+
+@pytest.mark.parametrize("eps,max_rank", [(0.0, 0), (1e-3, 0), (0.05, 0), (0.0, 5), (1e-2, 7), (0.3, 0)])
+def test_tt_svd_ranks_match_oracle(xe, ref, eps, max_rank):
+    """TT-SVD constructor (ttNetwork.cpp:112-160): eps / maxRank cuts give the oracle's ranks, and the
+    same tensor (the cut keeps the leading singular triplets; graded spectra keep gaps at the cuts)."""
+    rng = np.random.default_rng(41)
+    dims = [4, 5, 6, 5, 4]
+    # a TT with geometrically decaying core scales: distinct, well separated singular values per edge
+    ranks = [1, 4, 9, 9, 4, 1]
+    cores = [rng.standard_normal((ranks[k], dims[k], ranks[k + 1])) for k in range(5)]
+    for k in range(1, 5):
+        cores[k] = cores[k] * (0.5 ** np.arange(ranks[k]))[:, None, None]
+    full = ref.TT(cores).full()
+    full = full + 1e-9 * rng.standard_normal(full.shape)
+    mr = [max_rank] * 4
+    tt = xe.TTTensor(_tensor(xe, full), eps, max_rank)
+    o = ref.tt_svd(full, eps, mr)
+    assert tt.ranks() == o.ranks
+    got = xe.Tensor(tt).to_ndarray()
+    assert np.linalg.norm(got - o.full()) <= 1e-10 * np.linalg.norm(full)

@@ -51,7 +51,7 @@ void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, d
 // Right singular vectors of W (p x q, p <= min(q, 512); W[i][k] at W[i*ldw + k], or W[k*ldw + i] with
 // trans) by one-sided Jacobi on its rows (svd.hip): S (p) descending, Vt (p x q, row stride ldvt)
 // orthonormal rows, W = U S Vt with U S = W Vt^T. *status_dev = sweeps used, -1 if not converged in
-// max_sweeps, -2 if the block kernel's grid barrier timed out. kernel: 0 auto (p > 128: the
+// max_sweeps, -2 if the block kernel's grid barrier timed out. kernel: 0 auto (p >= 32: the
 // multi-workgroup block kernel, else one workgroup with W in LDS when p (q + 1) <= 18432 doubles),
 // 1 one workgroup, 2 blocks. Enqueued only.
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,

@@ -35,17 +35,18 @@ __device__ __forceinline__ double dpp(double v) {
     return __hiloint2double(hi, lo);
 }
 
-// Sum over a group of G (8 or 16) consecutive lanes. Every lane of the group ends with the same bits:
+// Sum over a group of G (8, 16 or 32) consecutive lanes. Every lane of the group ends with the same bits:
 // each step adds two values that are equal up to the order of operands of commutative adds.
 //   G = 16: row_ror 8, 4, 2, 1 (rotations of an increasingly periodic sequence)
 //   G = 8:  row_half_mirror (i <-> 7-i), quad_perm [2,3,0,1] (i <-> i^2), quad_perm [1,0,3,2] (i <-> i^1)
 template <int G>
 __device__ __forceinline__ double gsum(double v) {
-    if constexpr (G == 16) {
+    if constexpr (G == 16 || G == 32) {
         v += dpp<0x128>(v);
         v += dpp<0x124>(v);
         v += dpp<0x122>(v);
         v += dpp<0x121>(v);
+        if constexpr (G == 32) v += __shfl_xor(v, 16, 64);   // the two DPP rows of the group
     } else {
         static_assert(G == 8, "groups of 8 or 16 lanes");
         v += dpp<0x141>(v);
@@ -77,14 +78,29 @@ __device__ __forceinline__ double fsqrt(double x) {   // x > 0
 
 // Jacobi rotation zeroing the (i,j) entry of [[a c][c b]]: t = tan(theta) = sign(b - a) 2c /
 // (|b - a| + sqrt((b - a)^2 + 4 c^2)) (the smaller root), c = 1/sqrt(1+t^2), s = t c, tau = s / (1 + c)
-__device__ __forceinline__ void rotation(double a, double b, double c, double& s, double& tau) {
+__device__ __forceinline__ void rotation(double a, double b, double c, double& s, double& tau, double& tn) {
     const double dd = b - a;
     const double hh = fsqrt(fma(dd, dd, 4.0 * c * c));
-    const double tn = copysign(2.0, dd) * c * frcp(fabs(dd) + hh);
-    const double qq = fsqrt(fma(tn, tn, 1.0));
-    const double cs = frcp(qq);
-    s = tn * cs;
-    tau = s * frcp(1.0 + cs);   // Rutishauser: x' = x - s (y + tau x), y' = y + s (x - tau y)
+    tn = copysign(2.0, dd) * c * frcp(fabs(dd) + hh);
+    const double qq = fsqrt(fma(tn, tn, 1.0));   // 1 / cos
+    s = tn * frcp(qq);
+    tau = tn * frcp(1.0 + qq);   // = s / (1 + cos); Rutishauser: x' = x - s (y + tau x), y' = y + s (x - tau y)
+}
+__device__ __forceinline__ void rotation(double a, double b, double c, double& s, double& tau) {
+    double tn;
+    rotation(a, b, c, s, tau, tn);
+}
+
+// rows padded with zeros to E * G (no bounds checks: the padding stays zero under rotations)
+template <int G, int E>
+__device__ __forceinline__ void load_row_full(double (&x)[E], const double* __restrict__ w, int l) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) x[e] = w[l + e * G];
+}
+template <int G, int E>
+__device__ __forceinline__ void store_row_full(const double (&x)[E], double* __restrict__ w, int l) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) w[l + e * G] = x[e];
 }
 
 // One Jacobi step on the row pair (wi, wj) of length q by a group of G lanes (lane l): orthogonalise the
@@ -265,24 +281,30 @@ __global__ void __launch_bounds__(SVG_THREADS) k_jacobi_vt_global(double* __rest
 }
 
 
-// ---- multi-workgroup block Jacobi (p > 128): the rows are cut into nb blocks of SVB_ROWS (the last ones
+// ---- multi-workgroup block Jacobi (p >= 32): the rows are cut into nb blocks of BR rows (the last ones
 // padded with zero rows); workgroup w holds the block pair at positions (w, nb-1-w) of the circle
-// tournament over blocks -- 2 SVB_ROWS rows x q in LDS -- and orthogonalises its rows with one inner
-// sweep (2 SVB_ROWS - 1 rounds of SVB_ROWS disjoint pairs, a 16-lane group per pair); then every block
-// goes through global memory to the workgroup that pairs it next (one grid barrier per outer round).
-// nb - 1 outer rounds are one sweep; converged when a whole sweep rotated nothing.
-// Grid barrier: monotone counter; producer = every wave's vmcnt(0) + barrier + lane-0 agent release
-// fence, consumer = relaxed poll + agent acquire fence (MI355X_MICROARCH.md, inter-workgroup
-// visibility). The poll is bounded (status -2 instead of a hang if a workgroup were never scheduled).
-constexpr int SVB_ROWS = 16, SVB_G = 16, SVB_THREADS = SVB_ROWS * SVB_G, SVB_QMAX = 512;
+// tournament over blocks -- 2 BR rows x q in LDS, each block contiguous -- and per outer round
+// orthogonalises the BR x BR cross pairs (BR rounds of BR disjoint pairs, a 16-lane group per pair, the
+// group's top row register-resident); the pairs inside each block are done once per sweep, in its
+// first outer round. Then every block goes through global memory to the workgroup that pairs it next.
+// nb - 1 outer rounds are one sweep (every row pair exactly once); converged when a whole sweep rotated
+// nothing.
+// Hand-off between outer rounds (MI355X_MICROARCH.md, inter-workgroup visibility, row 1 of the sc1
+// table): every byte of a block is stored and loaded with 16-B write-through (sc1) buffer accesses,
+// every wave drains its stores (vmcnt(0)) before the workgroup barrier behind which lane 0 adds to the
+// grid counter (agent atomic), the poll is an sc1 load and the other waves load after the workgroup
+// barrier that the polling wave joins -- no release/acquire fences (no L2 write-back or L1 invalidate
+// per round). The poll is bounded (status -2 instead of a hang if a workgroup were never scheduled).
+constexpr int SVB_G = 16, SVB_LDS = 16384, SVB_QMAX = 512;
 constexpr int SVB_SYNC_WORDS = 64;   // [0] barrier counter, [1 + sweep] rotated flags
+typedef int svb_v4i __attribute__((ext_vector_type(4)));
+constexpr int kBufCfg = 0x00020000;  // raw buffer descriptor word 3 (32-bit data format)
+constexpr int kSc1 = 16;             // cache policy: sc1 (write-through stores, L1-bypassing loads)
 
-__device__ __forceinline__ void grid_barrier(unsigned* counter, unsigned target, int* err) {
+__device__ __forceinline__ void grid_arrive_wait(unsigned* counter, unsigned target, int* err) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
         while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -292,54 +314,78 @@ __device__ __forceinline__ void grid_barrier(unsigned* counter, unsigned target,
                 break;
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 }
 
-template <int E>
-__global__ void __launch_bounds__(SVB_THREADS) k_jacobi_vt_blocks(const double* __restrict__ Win, int ldin, int trans, int p, int q,
-                                                                  int nb, int max_sweeps, double* __restrict__ slots,
-                                                                  unsigned* __restrict__ sync, double* __restrict__ norms,
-                                                                  double* __restrict__ S, double* __restrict__ Vt, int ldvt,
-                                                                  int* __restrict__ status) {
-    constexpr int R2 = 2 * SVB_ROWS;
-    __shared__ double Ws[R2 * (SVB_QMAX + 1)];
+// LDS block (contiguous, 16-B aligned) <-> global slot, 16-B sc1 accesses, 4 per lane in flight
+template <int NT>
+__device__ __forceinline__ void block_out(const double* lds, __amdgpu_buffer_rsrc_t rs, int byte0, int units, int tid) {
+    for (int u0 = 0; u0 < units; u0 += 4 * NT) {
+        svb_v4i v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int u = u0 + i * NT + tid;
+            if (u < units) v[i] = *reinterpret_cast<const svb_v4i*>(lds + 2 * u);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int u = u0 + i * NT + tid;
+            if (u < units) __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, byte0 + 16 * u, 0, kSc1);
+        }
+    }
+}
+template <int NT>
+__device__ __forceinline__ void block_in(double* lds, __amdgpu_buffer_rsrc_t rs, int byte0, int units, int tid) {
+    for (int u0 = 0; u0 < units; u0 += 8 * NT) {
+        svb_v4i v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int u = u0 + i * NT + tid;
+            if (u < units) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, byte0 + 16 * u, 0, kSc1);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int u = u0 + i * NT + tid;
+            if (u < units) *reinterpret_cast<svb_v4i*>(lds + 2 * u) = v[i];
+        }
+    }
+}
+
+template <int BR, int G, int E>
+__global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __restrict__ Win, int ldin, int trans, int p, int q,
+                                                                 int nb, int max_sweeps, double* __restrict__ slots,
+                                                                 unsigned* __restrict__ sync, double* __restrict__ norms,
+                                                                 double* __restrict__ S, double* __restrict__ Vt, int ldvt,
+                                                                 int* __restrict__ status) {
+    constexpr int NT = BR * G, R2 = 2 * BR;
+    static_assert((BR & (BR - 1)) == 0 && BR >= 4, "BR: a power of two");
+    __shared__ __attribute__((aligned(16))) double Ws[SVB_LDS];
     __shared__ int rotated, err;
-    __shared__ int part[SVB_THREADS / 64];
-    const int tid = threadIdx.x, g = tid / SVB_G, l = tid % SVB_G;
+    __shared__ double bn[BR];   // squared norms of the bottom rows during the cross rounds
+    __shared__ int part[NT / 64 > 0 ? NT / 64 : 1];
+    const int tid = threadIdx.x, g = tid / G, l = tid % G;
     const int w = blockIdx.x, nwg = gridDim.x;
-    const int ldw = q + ((q & 1) ? 0 : 1);
+    constexpr int ldw = E * G;      // rows zero-padded to the register tiling; blocks contiguous
+    constexpr int bunits = BR * ldw / 2;   // 16-B units per block
+    static_assert(2 * BR * ldw <= SVB_LDS, "block pair exceeds the LDS buffer");
+    double* const Wb = Ws + BR * ldw;   // bottom block
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slots, 0, nb * BR * ldw * 8, kBufCfg);
     const double tol = sqrt(double(q)) * 1.1102230246251565e-16;
     const double tol2 = tol * tol;
     if (tid == 0) err = 0;
     // block id at tournament position x in outer round t
     auto block_at = [&](int x, int t) { return x == 0 ? 0 : 1 + (x - 1 + t) % (nb - 1); };
-    auto row_of = [&](int r, int top, int bot) { return (r < SVB_ROWS ? top : bot) * SVB_ROWS + (r % SVB_ROWS); };
-    auto load_blocks = [&](int top, int bot, bool from_input) {
-        for (int e = tid; e < R2 * q; e += SVB_THREADS) {
-            const int r = e / q, k = e - r * q;
-            const int row = row_of(r, top, bot);
-            double v = 0.0;
-            if (row < p) {
-                if (from_input) v = trans ? Win[size_t(k) * ldin + row] : Win[size_t(row) * ldin + k];
-                else v = slots[size_t(row) * q + k];
-            }
-            Ws[r * ldw + k] = v;
-        }
-    };
-    auto store_blocks = [&](int top, int bot) {
-        for (int e = tid; e < R2 * q; e += SVB_THREADS) {
-            const int r = e / q, k = e - r * q;
-            slots[size_t(row_of(r, top, bot)) * q + k] = Ws[r * ldw + k];
-        }
-    };
+    auto row_of = [&](int r, int top, int bot) { return (r < BR ? top : bot) * BR + (r % BR); };
     unsigned barriers = 0;
     long long t_bar = 0, t_xch = 0;
     const long long t_start = wall_clock64();
     int top = block_at(w, 0), bot = block_at(nb - 1 - w, 0);
-    load_blocks(top, bot, true);
+    for (int e = tid; e < R2 * ldw; e += NT) {
+        const int r = e / ldw, k = e % ldw;
+        const int row = row_of(r, top, bot);
+        Ws[e] = (row < p && k < q) ? (trans ? Win[size_t(k) * ldin + row] : Win[size_t(row) * ldin + k]) : 0.0;
+    }
     __syncthreads();
     int sweep = 0;
     bool converged = false;
@@ -348,47 +394,98 @@ __global__ void __launch_bounds__(SVB_THREADS) k_jacobi_vt_blocks(const double* 
         __syncthreads();
         for (int t = 0; t < nb - 1; ++t) {
             if (t == 0) {
-                // first outer round of the sweep: the pairs inside each block (circle method over
-                // SVB_ROWS rows; groups 0..7 on the top block, 8..15 on the bottom one)
-                constexpr int HALF = SVB_ROWS / 2;
-                const int gg = g % HALF, base = g < HALF ? 0 : SVB_ROWS;
-                for (int round = 0; round < SVB_ROWS - 1; ++round) {
-                    const int i = player(gg, round, SVB_ROWS), j = player(SVB_ROWS - 1 - gg, round, SVB_ROWS);
-                    if (rotate_pair<SVB_G, E>(Ws + (base + i) * ldw, Ws + (base + j) * ldw, q, l, tol2) && l == 0) rotated = 1;
-                    __syncthreads();
-                }
-            }
-            // the pairs across the two blocks: group g keeps top row g in registers and meets bottom row
-            // (g + s) mod SVB_ROWS in round s
-            {
-                double x[E], y[E];
-                load_row<SVB_G, E>(x, Ws + g * ldw, q, l);
-                bool rot = false;
-                for (int sr = 0; sr < SVB_ROWS; ++sr) {
-                    double* wb = Ws + (SVB_ROWS + ((g + sr) & (SVB_ROWS - 1))) * ldw;
-                    load_row<SVB_G, E>(y, wb, q, l);
-                    if (rotate_regs<SVB_G, E>(x, y, tol2)) {
-                        rot = true;
-                        store_row<SVB_G, E>(y, wb, q, l);
+                // first outer round of the sweep: the pairs inside each block (circle method over BR
+                // rows; the first half of the groups on the top block, the second on the bottom one)
+                constexpr int HALF = BR / 2;
+                const int gg = g % HALF, base = g < HALF ? 0 : BR;
+                for (int round = 0; round < BR - 1; ++round) {
+                    const int i = player(gg, round, BR), j = player(BR - 1 - gg, round, BR);
+                    double x[E], y[E];
+                    load_row_full<G, E>(x, Ws + (base + i) * ldw, l);
+                    load_row_full<G, E>(y, Ws + (base + j) * ldw, l);
+                    if (rotate_regs<G, E>(x, y, tol2)) {
+                        store_row_full<G, E>(x, Ws + (base + i) * ldw, l);
+                        store_row_full<G, E>(y, Ws + (base + j) * ldw, l);
+                        if (l == 0) rotated = 1;
                     }
                     __syncthreads();
                 }
-                store_row<SVB_G, E>(x, Ws + g * ldw, q, l);
+            }
+            // the cross pairs: group g keeps top row g in registers and meets bottom row (g + s) mod BR
+            // in round s. Squared norms are computed once per outer round and then updated with the
+            // rotation (a' = a - t c, b' = b + t c); a drop below half is recomputed (cancellation guard)
+            {
+                double x[E], y[E];
+                load_row_full<G, E>(x, Ws + g * ldw, l);
+                load_row_full<G, E>(y, Wb + g * ldw, l);
+                double a = 0.0, bb = 0.0;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    a = fma(x[e], x[e], a);
+                    bb = fma(y[e], y[e], bb);
+                }
+                a = gsum<G>(a);
+                bb = gsum<G>(bb);
+                if (l == 0) bn[g] = bb;
+                __syncthreads();
+                bool rot = false;
+                for (int sr = 0; sr < BR; ++sr) {
+                    const int jb = (g + sr) & (BR - 1);
+                    double* wb = Wb + jb * ldw;
+                    load_row_full<G, E>(y, wb, l);
+                    const double b = bn[jb];
+                    double c4[4] = {0.0, 0.0, 0.0, 0.0};   // four chains: the dot is latency-bound
+#pragma unroll
+                    for (int e = 0; e < E; ++e) c4[e & 3] = fma(x[e], y[e], c4[e & 3]);
+                    const double c = gsum<G>((c4[0] + c4[1]) + (c4[2] + c4[3]));
+                    if (c * c > tol2 * a * b) {
+                        double sn, tau, tn;
+                        rotation(a, b, c, sn, tau, tn);
+#pragma unroll
+                        for (int e = 0; e < E; ++e) {
+                            const double xe = x[e], ye = y[e];
+                            x[e] = xe - sn * fma(tau, xe, ye);
+                            y[e] = ye + sn * fma(-tau, ye, xe);
+                        }
+                        double an = fma(-tn, c, a), bnew = fma(tn, c, b);
+                        if (an < 0.5 * a) {
+                            an = 0.0;
+#pragma unroll
+                            for (int e = 0; e < E; ++e) an = fma(x[e], x[e], an);
+                            an = gsum<G>(an);
+                        }
+                        if (bnew < 0.5 * b) {
+                            bnew = 0.0;
+#pragma unroll
+                            for (int e = 0; e < E; ++e) bnew = fma(y[e], y[e], bnew);
+                            bnew = gsum<G>(bnew);
+                        }
+                        a = an;
+                        store_row_full<G, E>(y, wb, l);
+                        if (l == 0) bn[jb] = bnew;
+                        rot = true;
+                    }
+                    __syncthreads();
+                }
+                store_row_full<G, E>(x, Ws + g * ldw, l);
                 if (rot && l == 0) rotated = 1;
                 __syncthreads();
             }
-            // exchange: every block to the slot of its id, then the pair of the next outer round
+            // exchange: every block to the slot of its id, then the pair of the next outer round (block 0
+            // never leaves workgroup 0's top)
             const long long t0 = wall_clock64();
-            store_blocks(top, bot);
+            if (top != 0) block_out<NT>(Ws, rs, top * bunits * 16, bunits, tid);
+            block_out<NT>(Wb, rs, bot * bunits * 16, bunits, tid);
             if (t == nb - 2 && tid == 0 && rotated)
                 __hip_atomic_fetch_or(&sync[1 + sweep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const long long t1 = wall_clock64();
-            grid_barrier(&sync[0], ++barriers * unsigned(nwg), &err);
+            grid_arrive_wait(&sync[0], ++barriers * unsigned(nwg), &err);
             const long long t2 = wall_clock64();
             const int tn = (t + 1) % (nb - 1);
             top = block_at(w, tn);
             bot = block_at(nb - 1 - w, tn);
-            load_blocks(top, bot, false);
+            if (top != 0) block_in<NT>(Ws, rs, top * bunits * 16, bunits, tid);
+            block_in<NT>(Wb, rs, bot * bunits * 16, bunits, tid);
             __syncthreads();
             t_bar += t2 - t1;
             t_xch += (t1 - t0) + (wall_clock64() - t2);
@@ -401,23 +498,23 @@ __global__ void __launch_bounds__(SVB_THREADS) k_jacobi_vt_blocks(const double* 
         if (err) break;
         __syncthreads();
     }
-    // singular values = row norms; global ranks after one more barrier
-    for (int r = g; r < R2; r += SVB_ROWS) {
+    // singular values = row norms (published with sc1 stores); global ranks after one more barrier
+    for (int r = g; r < R2; r += BR) {
         const double* wr = Ws + r * ldw;
         double a = 0.0;
-        for (int k = l; k < q; k += SVB_G) a = fma(wr[k], wr[k], a);
-        a = gsum<SVB_G>(a);
+        for (int k = l; k < q; k += G) a = fma(wr[k], wr[k], a);
+        a = gsum<G>(a);
         const int row = row_of(r, top, bot);
-        if (l == 0 && row < p) norms[row] = sqrt(a);
+        if (l == 0 && row < p) __hip_atomic_store(&norms[row], sqrt(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    grid_barrier(&sync[0], ++barriers * unsigned(nwg), &err);
+    grid_arrive_wait(&sync[0], ++barriers * unsigned(nwg), &err);
     for (int r = 0; r < R2; ++r) {
         const int row = row_of(r, top, bot);
         if (row >= p) continue;
-        const double si = norms[row];
+        const double si = __hip_atomic_load(&norms[row], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int rk = 0;
-        for (int j2 = tid; j2 < p; j2 += SVB_THREADS) {
-            const double sj = norms[j2];
+        for (int j2 = tid; j2 < p; j2 += NT) {
+            const double sj = __hip_atomic_load(&norms[j2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             rk += (sj > si) || (sj == si && j2 < row);
         }
 #pragma unroll
@@ -426,11 +523,11 @@ __global__ void __launch_bounds__(SVB_THREADS) k_jacobi_vt_blocks(const double* 
         __syncthreads();
         int rank = 0;
 #pragma unroll
-        for (int i = 0; i < SVB_THREADS / 64; ++i) rank += part[i];
+        for (int i = 0; i < NT / 64; ++i) rank += part[i];
         __syncthreads();
         if (tid == 0) S[rank] = si;
         const double inv = si > 0.0 ? 1.0 / si : 0.0;
-        for (int k = tid; k < q; k += SVB_THREADS) Vt[size_t(rank) * ldvt + k] = Ws[r * ldw + k] * inv;
+        for (int k = tid; k < q; k += NT) Vt[size_t(rank) * ldvt + k] = Ws[r * ldw + k] * inv;
     }
     if (w == 0 && tid == 0) {
         status[0] = err ? -2 : (converged ? sweep : -1);
@@ -449,26 +546,28 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
     XRS_REQUIRE(p >= 1 && p <= SV_MAXP && p <= q, "jacobi_vt: need 1 <= p <= min(q, 512)");
     XRS_REQUIRE(kernel >= 0 && kernel <= 2, "jacobi_vt: kernel is 0 (auto), 1 (one workgroup) or 2 (blocks)");
     KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * q * 6.0, 16.0 * double(p) * q);
-    // smallest p handed to the multi-workgroup block kernel (XRS_SVD_BLOCK_MIN tunes it)
+    // smallest p handed to the multi-workgroup block kernel (XRS_SVD_BLOCK_MIN tunes it; measured faster
+    // than the one-workgroup kernel from p = 64 on: 0.59 vs 0.73 ms at 64, 1.19 vs 2.62 ms at 128)
     static const int block_min = [] {
         const char* e = std::getenv("XRS_SVD_BLOCK_MIN");
-        return e ? std::atoi(e) : 129;
+        return e ? std::atoi(e) : 32;
     }();
-    const bool blocks_ok = p > SVB_ROWS && q <= SVB_QMAX;
+    const bool blocks_ok = p > 16 && q <= SVB_QMAX;
     XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs 16 < p and q <= 512");
     if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
-        int nb = (p + SVB_ROWS - 1) / SVB_ROWS;
+        constexpr int BR = 16;
+        int nb = (p + BR - 1) / BR;
         nb += nb & 1;
         const int sweeps = std::min(max_sweeps, SVB_SYNC_WORDS - 1);
-        DevBuf slots(h, size_t(nb) * SVB_ROWS * q * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
+        DevBuf slots(h, size_t(nb) * BR * (q <= 256 ? 256 : 512) * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
         XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
-        // nb / 2 <= 16 one-CU workgroups: co-resident on any MI355X (the barrier needs all of them live)
+        // nb / 2 <= 16 one-CU workgroups: co-resident on any MI355X (the grid barrier needs all of them live)
         if (q <= 256)
-            hipLaunchKernelGGL(k_jacobi_vt_blocks<16>, dim3(nb / 2), dim3(SVB_THREADS), 0, h->stream, W, ldw, int(trans), p, q, nb,
-                               sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
+            hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, 32, 8>), dim3(nb / 2), dim3(BR * 32), 0, h->stream, W, ldw, int(trans), p, q,
+                               nb, sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
         else
-            hipLaunchKernelGGL(k_jacobi_vt_blocks<32>, dim3(nb / 2), dim3(SVB_THREADS), 0, h->stream, W, ldw, int(trans), p, q, nb,
-                               sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
+            hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, 32, 16>), dim3(nb / 2), dim3(BR * 32), 0, h->stream, W, ldw, int(trans), p, q,
+                               nb, sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
         check_launch("k_jacobi_vt_blocks");
     } else if (jacobi_vt_fits_lds(p, q)) {
         hipLaunchKernelGGL(k_jacobi_vt_lds, dim3(1), dim3(SVL_THREADS), 0, h->stream, W, ldw, int(trans), p, q, max_sweeps, S, Vt,
