@@ -397,8 +397,8 @@ def test_tt_svd_ranks_match_oracle(xe, ref, eps, max_rank):
         cores[k] = cores[k] * (0.5 ** np.arange(ranks[k]))[:, None, None]
     full = ref.TT(cores).full()
     full = full + 1e-9 * rng.standard_normal(full.shape)
-    mr = [max_rank] * 4
-    tt = xe.TTTensor(_tensor(xe, full), eps, max_rank)
+    mr = [max_rank] * 4   # oracle: 0 = no cap; the reference's default maxRank is size_t(-1)
+    tt = xe.TTTensor(_tensor(xe, full), eps, max_rank if max_rank else 2**63)
     o = ref.tt_svd(full, eps, mr)
     assert tt.ranks() == o.ranks
     got = xe.Tensor(tt).to_ndarray()

@@ -332,15 +332,23 @@ void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* 
 void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     XRS_REQUIRE(std::min(m, n) <= size_t(kSmallMax), "svd: min(m, n) > 512 not supported yet");
-    if (m <= n) {
-        jacobi_svd_rows(h, A, int(m), int(n), U, S, Vt);
+    if (m <= n && jacobi_usv_fits(int(m), int(n))) {
+        jacobi_svd_rows(h, A, int(m), int(n), U, S, Vt);   // rows of A directly
         return;
     }
-    DevBuf At(h, m * n * 8), Ut(h, n * n * 8), Vtt(h, n * m * 8);
-    transpose(h, At.d(), A, m, n);                                  // n x m
-    jacobi_svd_rows(h, At.d(), int(n), int(m), Ut.d(), S, Vtt.d());  // A^T = Ut S Vtt
-    transpose(h, U, Vtt.d(), n, m);                                  // U = Vtt^T (m x n)
-    transpose(h, Vt, Ut.d(), n, n);                                  // Vt = Ut^T
+    // preconditioned (the QR factor's rows are shorter and better conditioned for Jacobi):
+    //   wide A = R Q: R = U S Vr, Vt = Vr Q;   tall A = Q R: R = U_R S Vt, U = Q U_R
+    const size_t k = std::min(m, n);
+    DevBuf R(h, k * k * 8), Qf(h, m * n * 8), F(h, k * k * 8);
+    if (m <= n) {
+        rq(h, A, m, n, R.d(), Qf.d());
+        jacobi_svd_rows(h, R.d(), int(k), int(k), U, S, F.d());
+        gemm(h, Vt, k, n, 1.0, F.d(), k, false, k, Qf.d(), n, false);
+    } else {
+        qr(h, A, m, n, Qf.d(), R.d());
+        jacobi_svd_rows(h, R.d(), int(k), int(k), F.d(), S, Vt);
+        gemm(h, U, m, k, 1.0, Qf.d(), k, false, k, F.d(), k, false);
+    }
 }
 
 }  // namespace xrs

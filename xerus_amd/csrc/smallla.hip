@@ -15,6 +15,8 @@
 //             round-robin parallel ordering, rotations accumulated in J (U = J^T).
 #include "smallla.hpp"
 
+#include <cstdio>
+
 namespace xrs {
 
 constexpr int NB = 32;
@@ -1303,6 +1305,18 @@ size_t qrcp(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, doub
 
 void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, double* S, double* Vt) {
     XRS_REQUIRE(p >= 1 && p <= PMAX && p <= q, "jacobi_svd_rows: need 1 <= p <= min(q, 512)");
+    if (jacobi_usv_fits(p, q)) {
+        // multi-workgroup block Jacobi with the rotations accumulated (svd.hip); non-convergence is a
+        // warning, as the reference's dgesdd failure (blasLapackWrapper.cpp:216-224)
+        DevBuf st(h, 64);
+        jacobi_usv(h, W, q, false, p, q, U, p, S, Vt, q, st.as<int>(), 60);
+        int sweeps = 0;
+        read_status(h, st.as<int>(), 1, &sweeps);
+        if (sweeps < 0)
+            std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %d x %d matrix did not converge (status %d)\n",
+                         p, q, sweeps);
+        return;
+    }
     DevBuf Wc(h, size_t(p) * q * 8), J(h, size_t(p) * p * 8), st(h, 64);
     XRS_HIP(hipMemcpyAsync(Wc.d(), W, size_t(p) * q * 8, hipMemcpyDeviceToDevice, h->stream));
     {

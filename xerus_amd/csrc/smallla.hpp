@@ -57,6 +57,12 @@ void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, d
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
                int* status_dev, int max_sweeps = 40, int kernel = 0);
 bool jacobi_vt_fits_lds(int p, int q);
+// Full SVD of the rows of W (p x q, p <= q, 32 ceil(q/32) + p <= 1024) by the block Jacobi kernel with
+// the rotations accumulated (svd.hip): W = U diag(S) Vt, U p x p orthogonal (row stride ldu), S
+// descending, Vt p x q (orthonormal rows for S > 0). Status as jacobi_vt. Enqueued only.
+bool jacobi_usv_fits(int p, int q);
+void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
+                int* status_dev, int max_sweeps = 40);
 
 struct OrthResult {
     bool certified;   // sigma_min(A) >= cert_ratio * ||A||_F proven (Cholesky of the shifted Gram succeeded)

@@ -107,14 +107,17 @@ __device__ __forceinline__ void store_row_full(const double (&x)[E], double* __r
 // rows if |wi . wj| > tol ||wi|| ||wj||; true if rotated. E > 0: q <= E * G, the lane's elements are held
 // in registers (all loads issued before any use); E = 0: any q, streamed.
 // The register core: the lane's E elements of each row (zero beyond q, which rotations keep zero)
+// (the inner products run over the first ew elements: the rest may carry accumulated rotations)
 template <int G, int E>
-__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2) {
+__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E) {
     double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        a = fma(x[e], x[e], a);
-        b = fma(y[e], y[e], b);
-        c = fma(x[e], y[e], c);
+        if (e < ew) {
+            a = fma(x[e], x[e], a);
+            b = fma(y[e], y[e], b);
+            c = fma(x[e], y[e], c);
+        }
     }
     a = gsum<G>(a);
     b = gsum<G>(b);
@@ -352,12 +355,12 @@ __device__ __forceinline__ void block_in(double* lds, __amdgpu_buffer_rsrc_t rs,
     }
 }
 
-template <int BR, int G, int E>
+template <int BR, int G, int E, bool ACC>
 __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __restrict__ Win, int ldin, int trans, int p, int q,
                                                                  int nb, int max_sweeps, double* __restrict__ slots,
                                                                  unsigned* __restrict__ sync, double* __restrict__ norms,
                                                                  double* __restrict__ S, double* __restrict__ Vt, int ldvt,
-                                                                 int* __restrict__ status) {
+                                                                 double* __restrict__ U, int ldu, int* __restrict__ status) {
     constexpr int NT = BR * G, R2 = 2 * BR;
     static_assert((BR & (BR - 1)) == 0 && BR >= 4, "BR: a power of two");
     __shared__ __attribute__((aligned(16))) double Ws[SVB_LDS];
@@ -371,6 +374,10 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
     static_assert(2 * BR * ldw <= SVB_LDS, "block pair exceeds the LDS buffer");
     double* const Wb = Ws + BR * ldw;   // bottom block
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slots, 0, nb * BR * ldw * 8, kBufCfg);
+    // with U: every row carries its row of the accumulated rotation J (W' = J W) after the zero-padded
+    // data, [w (ew * G) | j (p)]; dots and norms run over the first ew register elements only
+    const int ew = ACC ? (q + G - 1) / G : E;
+    const int qpad = ew * G;
     const double tol = sqrt(double(q)) * 1.1102230246251565e-16;
     const double tol2 = tol * tol;
     if (tid == 0) err = 0;
@@ -384,7 +391,12 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
     for (int e = tid; e < R2 * ldw; e += NT) {
         const int r = e / ldw, k = e % ldw;
         const int row = row_of(r, top, bot);
-        Ws[e] = (row < p && k < q) ? (trans ? Win[size_t(k) * ldin + row] : Win[size_t(row) * ldin + k]) : 0.0;
+        double v = 0.0;
+        if (row < p) {
+            if (k < q) v = trans ? Win[size_t(k) * ldin + row] : Win[size_t(row) * ldin + k];
+            else if (ACC && k - qpad == row) v = 1.0;
+        }
+        Ws[e] = v;
     }
     __syncthreads();
     int sweep = 0;
@@ -403,7 +415,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                     double x[E], y[E];
                     load_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                     load_row_full<G, E>(y, Ws + (base + j) * ldw, l);
-                    if (rotate_regs<G, E>(x, y, tol2)) {
+                    if (rotate_regs<G, E>(x, y, tol2, ew)) {
                         store_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                         store_row_full<G, E>(y, Ws + (base + j) * ldw, l);
                         if (l == 0) rotated = 1;
@@ -421,8 +433,10 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                 double a = 0.0, bb = 0.0;
 #pragma unroll
                 for (int e = 0; e < E; ++e) {
-                    a = fma(x[e], x[e], a);
-                    bb = fma(y[e], y[e], bb);
+                    if (e < ew) {
+                        a = fma(x[e], x[e], a);
+                        bb = fma(y[e], y[e], bb);
+                    }
                 }
                 a = gsum<G>(a);
                 bb = gsum<G>(bb);
@@ -436,7 +450,8 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                     const double b = bn[jb];
                     double c4[4] = {0.0, 0.0, 0.0, 0.0};   // four chains: the dot is latency-bound
 #pragma unroll
-                    for (int e = 0; e < E; ++e) c4[e & 3] = fma(x[e], y[e], c4[e & 3]);
+                    for (int e = 0; e < E; ++e)
+                        if (e < ew) c4[e & 3] = fma(x[e], y[e], c4[e & 3]);
                     const double c = gsum<G>((c4[0] + c4[1]) + (c4[2] + c4[3]));
                     if (c * c > tol2 * a * b) {
                         double sn, tau, tn;
@@ -451,13 +466,15 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                         if (an < 0.5 * a) {
                             an = 0.0;
 #pragma unroll
-                            for (int e = 0; e < E; ++e) an = fma(x[e], x[e], an);
+                            for (int e = 0; e < E; ++e)
+                                if (e < ew) an = fma(x[e], x[e], an);
                             an = gsum<G>(an);
                         }
                         if (bnew < 0.5 * b) {
                             bnew = 0.0;
 #pragma unroll
-                            for (int e = 0; e < E; ++e) bnew = fma(y[e], y[e], bnew);
+                            for (int e = 0; e < E; ++e)
+                                if (e < ew) bnew = fma(y[e], y[e], bnew);
                             bnew = gsum<G>(bnew);
                         }
                         a = an;
@@ -502,7 +519,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
     for (int r = g; r < R2; r += BR) {
         const double* wr = Ws + r * ldw;
         double a = 0.0;
-        for (int k = l; k < q; k += G) a = fma(wr[k], wr[k], a);
+        for (int k = l; k < qpad; k += G) a = fma(wr[k], wr[k], a);
         a = gsum<G>(a);
         const int row = row_of(r, top, bot);
         if (l == 0 && row < p) __hip_atomic_store(&norms[row], sqrt(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -528,6 +545,8 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
         if (tid == 0) S[rank] = si;
         const double inv = si > 0.0 ? 1.0 / si : 0.0;
         for (int k = tid; k < q; k += NT) Vt[size_t(rank) * ldvt + k] = Ws[r * ldw + k] * inv;
+        if (ACC)   // W = J^T W': U = J^T, column `rank` = row r of J
+            for (int i2 = tid; i2 < p; i2 += NT) U[size_t(i2) * ldu + rank] = Ws[r * ldw + qpad + i2];
     }
     if (w == 0 && tid == 0) {
         status[0] = err ? -2 : (converged ? sweep : -1);
@@ -541,6 +560,25 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
 
 bool jacobi_vt_fits_lds(int p, int q) { return q <= 128 && size_t(p) * size_t(q + 1) <= size_t(SV_LDS); }
 
+namespace {
+
+// block kernel launch: nb = ceil(p / BR) rounded up to even, nb / 2 one-CU workgroups (<= 32 here:
+// co-resident on any MI355X, which the grid barrier needs)
+template <int BR, int G, int E, bool ACC>
+void launch_blocks(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt, double* U,
+                   int ldu, int* status_dev, int max_sweeps) {
+    int nb = (p + BR - 1) / BR;
+    nb += nb & 1;
+    const int sweeps = std::min(max_sweeps, SVB_SYNC_WORDS - 1);
+    DevBuf slots(h, size_t(nb) * BR * E * G * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
+    XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
+    hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, G, E, ACC>), dim3(nb / 2), dim3(BR * G), 0, h->stream, W, ldw, int(trans), p, q, nb, sweeps,
+                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev);
+    check_launch("k_jacobi_vt_blocks");
+}
+
+}  // namespace
+
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
                int* status_dev, int max_sweeps, int kernel) {
     XRS_REQUIRE(p >= 1 && p <= SV_MAXP && p <= q, "jacobi_vt: need 1 <= p <= min(q, 512)");
@@ -552,23 +590,11 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
         const char* e = std::getenv("XRS_SVD_BLOCK_MIN");
         return e ? std::atoi(e) : 32;
     }();
-    const bool blocks_ok = p > 16 && q <= SVB_QMAX;
-    XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs 16 < p and q <= 512");
+    const bool blocks_ok = q <= SVB_QMAX;
+    XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 512");
     if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
-        constexpr int BR = 16;
-        int nb = (p + BR - 1) / BR;
-        nb += nb & 1;
-        const int sweeps = std::min(max_sweeps, SVB_SYNC_WORDS - 1);
-        DevBuf slots(h, size_t(nb) * BR * (q <= 256 ? 256 : 512) * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
-        XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
-        // nb / 2 <= 16 one-CU workgroups: co-resident on any MI355X (the grid barrier needs all of them live)
-        if (q <= 256)
-            hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, 32, 8>), dim3(nb / 2), dim3(BR * 32), 0, h->stream, W, ldw, int(trans), p, q,
-                               nb, sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
-        else
-            hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, 32, 16>), dim3(nb / 2), dim3(BR * 32), 0, h->stream, W, ldw, int(trans), p, q,
-                               nb, sweeps, slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, status_dev);
-        check_launch("k_jacobi_vt_blocks");
+        if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+        else launch_blocks<16, 32, 16, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
     } else if (jacobi_vt_fits_lds(p, q)) {
         hipLaunchKernelGGL(k_jacobi_vt_lds, dim3(1), dim3(SVL_THREADS), 0, h->stream, W, ldw, int(trans), p, q, max_sweeps, S, Vt,
                            ldvt, status_dev);
@@ -579,6 +605,17 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
                            S, Vt, ldvt, status_dev);
         check_launch("k_jacobi_vt_global");
     }
+}
+
+bool jacobi_usv_fits(int p, int q) { return p >= 1 && p <= q && 32 * ((q + 31) / 32) + p <= 1024; }
+
+void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
+                int* status_dev, int max_sweeps) {
+    XRS_REQUIRE(jacobi_usv_fits(p, q), "jacobi_usv: need p <= q and 32 ceil(q / 32) + p <= 1024");
+    KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * (q + p) * 6.0, 16.0 * double(p) * (q + p));
+    const int width = 32 * ((q + 31) / 32) + p;
+    if (width <= 512) launch_blocks<16, 32, 16, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
+    else launch_blocks<8, 32, 32, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
 }
 
 }  // namespace xrs
