@@ -92,6 +92,9 @@ class TTTensor {
     IndexedTensor<TTTensor> operator()(const std::vector<Index>& _indices) const;
     template <typename... args>
     IndexedTensor<TTTensor> operator()(args... _args) const;
+    IndexedTensor<TTTensor> operator()(const std::vector<Index>& _indices);
+    template <typename... args>
+    IndexedTensor<TTTensor> operator()(args... _args);
 
     void require_correct_format() const;
 };
@@ -111,7 +114,10 @@ template <>
 class IndexedTensor<TTTensor> {
    public:
     const TTTensor* tt;
+    TTTensor* mut = nullptr;   // set when indexed through a non-const TTTensor (assignment target)
     std::vector<Index> indices;
+    /// y(i&0) = A(i/2, j/2) * x(j&0) (and the transposed x^T A form), ttNetwork.cpp:1075-1093
+    IndexedTensor& operator=(const class IndexedTTStack& _stack);
 };
 
 class IndexedTTProduct {
@@ -128,7 +134,140 @@ template <typename... args>
 IndexedTensor<TTTensor> TTTensor::operator()(args... _args) const {
     return (*this)(std::vector<Index>({Index(_args)...}));
 }
+template <typename... args>
+IndexedTensor<TTTensor> TTTensor::operator()(args... _args) {
+    return (*this)(std::vector<Index>({Index(_args)...}));
+}
 
 using TTNetwork = TTTensor;
+
+// ------------------------------------------------------------------------------------------ TTOperator
+class TTOperator;
+template <>
+class IndexedTensor<TTOperator>;
+
+/// TTOperator (= TTNetwork<true>, ttNetwork.h:46-519 with N = 2): component k has dims
+/// (r_k, n_k, m_k, r_{k+1}); dimensions = (n_0..n_{d-1}, m_0..m_{d-1}). Storage-wise a TTOperator is the
+/// TTTensor with modes n_k m_k (the same row-major cores), so canonicalisation, rounding, sums and norms
+/// run through the TT drivers on that view; application to a TTTensor / TTOperator is the TTStack
+/// contraction (xrs_tt_operator_apply).
+class TTOperator {
+   public:
+    std::vector<Tensor> components;
+    std::vector<size_t> dimensions;
+    bool canonicalized = true;
+    size_t corePosition = 0;
+
+    TTOperator();
+    /// all-zero operator of rank 1 (ttNetwork.cpp:57-108)
+    explicit TTOperator(const Tensor::DimensionTuple& _dimensions);
+    explicit TTOperator(size_t _degree);
+    /// TT-SVD of a dense operator tensor (i_0..i_{d-1}, j_0..j_{d-1}) (ttNetwork.cpp:111-160, N = 2)
+    explicit TTOperator(const Tensor& _tensor, const double _eps = EPSILON,
+                        const size_t _maxRank = std::numeric_limits<size_t>::max());
+    TTOperator(const Tensor& _tensor, const double _eps, const std::vector<size_t>& _maxRanks);
+
+    template <class distribution = std::normal_distribution<value_t>, class generator = std::mt19937_64>
+    static TTOperator random(std::vector<size_t> _dimensions, const std::vector<size_t>& _ranks,
+                             distribution& _dist = misc::defaultNormalDistribution, generator& _rnd = misc::randomEngine) {
+        TTOperator result = from_tt(TTTensor::random(merged_dimensions(_dimensions), _ranks, _dist, _rnd), _dimensions);
+        return result;
+    }
+    template <class distribution = std::normal_distribution<value_t>, class generator = std::mt19937_64>
+    static TTOperator random(std::vector<size_t> _dimensions, const size_t _rank,
+                             distribution& _dist = misc::defaultNormalDistribution, generator& _rnd = misc::randomEngine) {
+        return random(_dimensions, std::vector<size_t>(_dimensions.size() < 2 ? 0 : _dimensions.size() / 2 - 1, _rank), _dist, _rnd);
+    }
+    /// identity operator, cores delta(i, j), then canonicalize_left (ttNetwork.cpp:194-221)
+    static TTOperator identity(const std::vector<size_t>& _dimensions);
+    /// all-ones operator (ttNetwork.cpp:169-191)
+    static TTOperator ones(const std::vector<size_t>& _dimensions);
+
+    size_t degree() const { return dimensions.size(); }
+    std::vector<size_t> ranks() const;
+    size_t rank(const size_t _i) const;
+    const Tensor& get_component(const size_t _idx) const { return components.at(_idx); }
+    Tensor& component(const size_t _idx);
+    void set_component(const size_t _idx, Tensor _T);
+
+    void move_core(const size_t _position, const bool _keepRank = false);
+    void canonicalize_left() { move_core(0); }
+    void canonicalize_right() { move_core(degree() < 2 ? 0 : degree() / 2 - 1); }
+    void assume_core_position(const size_t _pos);
+    void round(const std::vector<size_t>& _maxRanks, const double _eps = EPSILON);
+    void round(const size_t _maxRank);
+    void round(const int _maxRank);
+    void round(const value_t _eps);
+    value_t frob_norm() const;
+    /// swaps row and column modes (ttNetwork.h:443-448)
+    void transpose();
+
+    TTOperator& operator+=(const TTOperator& _other);
+    TTOperator& operator-=(const TTOperator& _other);
+    TTOperator& operator*=(const value_t _factor);
+    TTOperator& operator/=(const value_t _divisor);
+
+    operator Tensor() const;
+    Tensor to_tensor() const;
+
+    IndexedTensor<TTOperator> operator()(const std::vector<Index>& _indices) const;
+    IndexedTensor<TTOperator> operator()(const std::vector<Index>& _indices);
+    template <typename... args>
+    IndexedTensor<TTOperator> operator()(args... _args) const;
+    template <typename... args>
+    IndexedTensor<TTOperator> operator()(args... _args);
+
+    void require_correct_format() const;
+
+    // the TTTensor view (modes n_k m_k) and back
+    static std::vector<size_t> merged_dimensions(const std::vector<size_t>& _dimensions);
+    TTTensor to_tt() &&;
+    static TTOperator from_tt(TTTensor&& _tt, const std::vector<size_t>& _dimensions);
+};
+
+TTOperator operator+(TTOperator _lhs, const TTOperator& _rhs);
+TTOperator operator-(TTOperator _lhs, const TTOperator& _rhs);
+TTOperator operator*(const value_t _factor, TTOperator _op);
+TTOperator operator*(TTOperator _op, const value_t _factor);
+TTOperator operator/(TTOperator _op, const value_t _divisor);
+inline value_t frob_norm(const TTOperator& _op) { return _op.frob_norm(); }
+
+template <>
+class IndexedTensor<TTOperator> {
+   public:
+    const TTOperator* op;
+    TTOperator* mut = nullptr;
+    std::vector<Index> indices;
+    /// C(i/2, k/2) = A(i/2, j/2) * B(j/2, k/2)
+    IndexedTensor& operator=(const class IndexedTTStack& _stack);
+};
+
+/// A lazily contracted operator application (reference: TTStack, ttStack.h / ttStack.cpp): A x,
+/// x^T A (x(i&0) * A(i/2, j/2)) or A B. Evaluated on assignment, or as a scalar against a TTTensor.
+class IndexedTTStack {
+   public:
+    const TTOperator* op = nullptr;
+    const TTTensor* vec = nullptr;        // A x / x^T A
+    const TTOperator* rhsOp = nullptr;    // A B
+    bool transposed = false;              // x^T A
+    std::vector<Index> indices;           // the free indices of the result
+    /// the contracted TTStack (TTTensor result), canonicalised at the operator's core (ttStack.cpp:160-168)
+    TTTensor evaluate_tt() const;
+    TTOperator evaluate_op() const;
+};
+IndexedTTStack operator*(const IndexedTensor<TTOperator>& _a, const IndexedTensor<TTTensor>& _x);
+IndexedTTStack operator*(const IndexedTensor<TTTensor>& _x, const IndexedTensor<TTOperator>& _a);
+IndexedTTStack operator*(const IndexedTensor<TTOperator>& _a, const IndexedTensor<TTOperator>& _b);
+/// value_t(x(i&0) * A(i/2, j/2) * y(j&0)) and value_t(A(i/2, j/2) * x(j&0) * y(i&0))
+value_t operator*(const IndexedTTStack& _s, const IndexedTensor<TTTensor>& _y);
+
+template <typename... args>
+IndexedTensor<TTOperator> TTOperator::operator()(args... _args) const {
+    return (*this)(std::vector<Index>({Index(_args)...}));
+}
+template <typename... args>
+IndexedTensor<TTOperator> TTOperator::operator()(args... _args) {
+    return (*this)(std::vector<Index>({Index(_args)...}));
+}
 
 }  // namespace xerus

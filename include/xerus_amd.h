@@ -149,6 +149,17 @@ int xrs_tt_move_core(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, 
  *  sigma_j <= eps*sigma_0 (tensor.cpp:1463-1474). On return the core is at position 0. */
 int xrs_tt_round(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
                  int canonicalized, size_t core_position, const size_t* max_ranks, double eps);
+/** TTOperator application, the core-wise contraction of a TTStack (ttStack.cpp:197-309, built by
+ *  TTNetwork<true>::specialized_contraction_f, ttNetwork.cpp:886-967). Operator A: cores
+ *  (ra[k], n[k], m[k], ra[k+1]). With p == NULL, B is a TTTensor with cores (rb[k], m[k], rb[k+1]) and
+ *  out[k] = (ra[k] rb[k], n[k], ra[k+1] rb[k+1]) holds sum_j A[a,i,j,a'] B[b,j,b'] (y = A x); with
+ *  transpose_a the row mode is contracted instead (x^T A: B cores (rb[k], n[k], rb[k+1]), out modes m[k]).
+ *  With p != NULL, B is an operator with cores (rb[k], m[k], p[k], rb[k+1]) and out[k] is the operator
+ *  core (ra rb, n, p, ra' rb') of A B. Fused ranks (a, b), the operator's index major. The output cores
+ *  are allocated from the handle's pool (release with xrs_free). No canonicalisation: the reference
+ *  then moves the core to the operator's core position (ttStack.cpp:163-166), xrs_tt_move_core. */
+int xrs_tt_operator_apply(xrs_handle_t handle, size_t d, const size_t* n, const size_t* m, const size_t* p, const size_t* ra,
+                          const double* const* A, const size_t* rb, const double* const* B, int transpose_a, double** out);
 /** Which algorithm the handle's last xrs_tt_round used: XRS_ROUND_CHAIN (certified, no cut possible:
  *  Gram chains + batched factorisations), XRS_ROUND_TRUNCATE (certified truncation: left chain pass +
  *  device-resident right-to-left SVD sweep), XRS_ROUND_REFERENCE (the reference's sequential

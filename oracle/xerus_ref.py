@@ -412,3 +412,40 @@ def tt_add(x: TT, y: TT) -> TT:
             Z[a1:, :, b1:] = Y
             cores.append(Z)
     return TT(cores)
+
+
+# ------------------------------------------------------------------------------------------------
+# TTOperator (TTNetwork<true>): core k has dims (r_k, n_k, m_k, r_{k+1}); dense form (n_0..n_{d-1}, m_0..m_{d-1}).
+def op_full(cores: Sequence[np.ndarray]) -> np.ndarray:
+    """Contract the operator cores and order the modes (i_0..i_{d-1}, j_0..j_{d-1}) (TTNetwork<true> layout,
+    ttNetwork.cpp:70-100)."""
+    d = len(cores)
+    res = cores[0]
+    for c in cores[1:]:
+        res = np.tensordot(res, c, axes=([res.ndim - 1], [0]))
+    res = res.reshape([s for c in cores for s in c.shape[1:3]])
+    return np.ascontiguousarray(np.transpose(res, [2 * k for k in range(d)] + [2 * k + 1 for k in range(d)]))
+
+
+def op_apply_cores(A: Sequence[np.ndarray], X: Sequence[np.ndarray], transpose: bool = False) -> List[np.ndarray]:
+    """The contracted TTStack of A(i/2, j/2) * x(j&0) (ttStack.cpp:197-309): core k is
+    C[(a,b), i, (a',b')] = sum_j A[a,i,j,a'] X[b,j,b'], fused ranks operator-major (the operator's node is
+    contracted first, :216-228); transpose: x(i&0) * A(i/2, j/2), the row mode contracted."""
+    out = []
+    for Ak, Xk in zip(A, X):
+        ra, n, m, ra2 = Ak.shape
+        rb, _, rb2 = Xk.shape
+        C = np.einsum('aijd,bic->abjdc', Ak, Xk) if transpose else np.einsum('aijd,bjc->abidc', Ak, Xk)
+        out.append(np.ascontiguousarray(C.reshape(ra * rb, C.shape[2], ra2 * rb2)))
+    return out
+
+
+def op_op_cores(A: Sequence[np.ndarray], B: Sequence[np.ndarray]) -> List[np.ndarray]:
+    """A(i/2, j/2) * B(j/2, k/2): C[(a,b), i, k, (a',b')] = sum_j A[a,i,j,a'] B[b,j,k,b'] (ttStack.cpp:197-309)."""
+    out = []
+    for Ak, Bk in zip(A, B):
+        ra, n, m, ra2 = Ak.shape
+        rb, _, p, rb2 = Bk.shape
+        C = np.einsum('aijd,bjkc->abikdc', Ak, Bk)
+        out.append(np.ascontiguousarray(C.reshape(ra * rb, n, p, ra2 * rb2)))
+    return out

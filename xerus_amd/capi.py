@@ -51,6 +51,8 @@ SIGNATURES = {
     "xrs_rq": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
     "xrs_svd": (C.c_int, [_DP, _DP, _DP, _DP, _DP, _SZ, _SZ]),
     "xrs_svd_rows_vt": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ, C.c_int]),
+    "xrs_tt_operator_apply": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
+                                        C.POINTER(_SZ), C.POINTER(_DP), C.c_int, C.POINTER(_DP)]),
     "xrs_tt_move_core": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ, _SZ, C.c_int]),
     "xrs_tt_round": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ,
                                C.POINTER(_SZ), C.c_double]),
@@ -269,6 +271,24 @@ class Handle:
         S, Vt, sw = self.empty((p,)), self.empty((p, q)), C.c_int()
         _check("xrs_svd_rows_vt", self.lib.xrs_svd_rows_vt(self.h, _DP(S.ptr), _DP(Vt.ptr), C.byref(sw), _DP(A.ptr), p, q, kernel))
         return S, Vt, sw.value
+
+    def tt_operator_apply(self, n, m, ra, A, rb, B, p=None, transpose=False):
+        """xrs_tt_operator_apply on device cores (DeviceArrays); returns the product cores as numpy arrays
+        (the device results are freed)."""
+        d = len(n)
+        out = (_DP * d)()
+        tab = lambda xs: (_DP * d)(*[_DP(x.ptr) for x in xs])  # noqa: E731
+        _check("xrs_tt_operator_apply", self.lib.xrs_tt_operator_apply(
+            self.h, d, _arr(n), _arr(m), _arr(p) if p is not None else None, _arr(ra), tab(A), _arr(rb), tab(B),
+            int(transpose), out))
+        res = []
+        for k in range(d):
+            nk = m[k] if transpose else n[k]
+            shape = (ra[k] * rb[k], nk) + ((p[k],) if p is not None else ()) + (ra[k + 1] * rb[k + 1],)
+            arr = DeviceArray(self, shape, ptr=out[k], owned=False)
+            res.append(arr.numpy())
+            self.free(out[k])
+        return res
 
     def last_round_path(self) -> str | None:
         """"chain" / "truncate" / "reference": the algorithm of this handle's last TT round."""

@@ -126,6 +126,7 @@ PYBIND11_MODULE(xerus, m) {
     py::class_<Tensor>(m, "Tensor")
         .def(py::init<>())
         .def(py::init([](const TTTensor& _tt) { return _tt.to_tensor(); }))
+        .def(py::init([](const TTOperator& _op) { return _op.to_tensor(); }))
         .def(py::init([](const std::vector<size_t>& _dims) { return Tensor(_dims); }))
         .def_static("from_ndarray", &from_ndarray)
         .def("to_ndarray", &to_ndarray)
@@ -226,13 +227,22 @@ PYBIND11_MODULE(xerus, m) {
     m.def("file_type", &misc::file_type);
 
     // ------------------------------------------------------------------ TTTensor
+    py::class_<IndexedTTStack>(m, "IndexedTTStack")
+        .def("__mul__", [](const IndexedTTStack& _s, const IndexedTensor<TTTensor>& _y) { return _s * _y; });
+    py::class_<IndexedTensor<TTOperator>>(m, "IndexedTTOperator")
+        .def("__mul__", [](const IndexedTensor<TTOperator>& _a, const IndexedTensor<TTTensor>& _x) { return _a * _x; })
+        .def("__mul__", [](const IndexedTensor<TTOperator>& _a, const IndexedTensor<TTOperator>& _b) { return _a * _b; })
+        .def("__lshift__", [](IndexedTensor<TTOperator>& _l, const IndexedTTStack& _r) { _l = _r; });
     py::class_<IndexedTensor<TTTensor>>(m, "IndexedTTTensor")
-        .def("__mul__", [](const IndexedTensor<TTTensor>& _a, const IndexedTensor<TTTensor>& _b) { return _a * _b; });
+        .def("__mul__", [](const IndexedTensor<TTTensor>& _a, const IndexedTensor<TTTensor>& _b) { return _a * _b; })
+        .def("__mul__", [](const IndexedTensor<TTTensor>& _x, const IndexedTensor<TTOperator>& _a) { return _x * _a; })
+        .def("__lshift__", [](IndexedTensor<TTTensor>& _l, const IndexedTTStack& _r) { _l = _r; });
     py::class_<IndexedTTProduct>(m, "IndexedTTProduct")
         .def("__float__", [](const IndexedTTProduct& _p) { return value_t(_p); });
 
     py::class_<TTTensor>(m, "TTTensor")
         .def(py::init<>())
+        .def(py::init<const TTTensor&>())
         .def(py::init([](const Tensor& _t, value_t _eps, size_t _maxRank) { return TTTensor(_t, _eps, _maxRank); }), py::arg("tensor"),
              py::arg("eps") = EPSILON, py::arg("maxRank") = std::numeric_limits<size_t>::max())
         .def(py::init([](const Tensor& _t, value_t _eps, const std::vector<size_t>& _maxRanks) { return TTTensor(_t, _eps, _maxRanks); }))
@@ -261,7 +271,7 @@ PYBIND11_MODULE(xerus, m) {
         .def("round", py::overload_cast<const value_t>(&TTTensor::round))
         .def("frob_norm", &TTTensor::frob_norm)
         .def("exceeds_maximal_ranks", &TTTensor::exceeds_maximal_ranks)
-        .def("__call__", [](const TTTensor& _t, py::args _a) { return _t(to_indices(_a)); }, py::keep_alive<0, 1>())
+        .def("__call__", [](TTTensor& _t, py::args _a) { return _t(to_indices(_a)); }, py::keep_alive<0, 1>())
         .def(py::self + py::self)
         .def(py::self - py::self)
         .def(py::self += py::self)
@@ -271,6 +281,46 @@ PYBIND11_MODULE(xerus, m) {
         .def(py::self / value_t())
         .def("__copy__", [](const TTTensor& _t) { return TTTensor(_t); });
     m.def("dot", [](const TTTensor& _x, const TTTensor& _y) { return dot(_x, _y); });
+
+    // ------------------------------------------------------------------ TTOperator (TTNetwork<true>)
+    py::class_<TTOperator>(m, "TTOperator")
+        .def(py::init<>())
+        .def(py::init<const TTOperator&>())
+        .def(py::init([](const Tensor& _t, value_t _eps, size_t _maxRank) { return TTOperator(_t, _eps, _maxRank); }), py::arg("tensor"),
+             py::arg("eps") = EPSILON, py::arg("maxRank") = std::numeric_limits<size_t>::max())
+        .def(py::init([](const Tensor& _t, value_t _eps, const std::vector<size_t>& _maxRanks) { return TTOperator(_t, _eps, _maxRanks); }))
+        .def(py::init([](const std::vector<size_t>& _dims) { return TTOperator(_dims); }))
+        .def(py::init([](size_t _degree) { return TTOperator(_degree); }))
+        .def_static("random", [](const std::vector<size_t>& _dims, const std::vector<size_t>& _ranks) { return TTOperator::random(_dims, _ranks); })
+        .def_static("random", [](const std::vector<size_t>& _dims, size_t _rank) { return TTOperator::random(_dims, _rank); })
+        .def_static("identity", &TTOperator::identity)
+        .def_static("ones", &TTOperator::ones)
+        .def_readonly("dimensions", &TTOperator::dimensions)
+        .def_readonly("canonicalized", &TTOperator::canonicalized)
+        .def_readonly("corePosition", &TTOperator::corePosition)
+        .def("degree", &TTOperator::degree)
+        .def("ranks", &TTOperator::ranks)
+        .def("rank", &TTOperator::rank)
+        .def("get_component", &TTOperator::get_component)
+        .def("set_component", &TTOperator::set_component)
+        .def("move_core", &TTOperator::move_core, py::arg("position"), py::arg("keepRank") = false)
+        .def("canonicalize_left", &TTOperator::canonicalize_left)
+        .def("canonicalize_right", &TTOperator::canonicalize_right)
+        .def("round", py::overload_cast<const std::vector<size_t>&, const double>(&TTOperator::round), py::arg("maxRanks"),
+             py::arg("eps") = EPSILON)
+        .def("round", py::overload_cast<const size_t>(&TTOperator::round))
+        .def("round", py::overload_cast<const value_t>(&TTOperator::round))
+        .def("frob_norm", &TTOperator::frob_norm)
+        .def("transpose", &TTOperator::transpose)
+        .def("__call__", [](TTOperator& _t, py::args _a) { return _t(to_indices(_a)); }, py::keep_alive<0, 1>())
+        .def(py::self + py::self)
+        .def(py::self - py::self)
+        .def(py::self += py::self)
+        .def(py::self -= py::self)
+        .def(py::self * value_t())
+        .def(value_t() * py::self)
+        .def(py::self / value_t())
+        .def("__copy__", [](const TTOperator& _t) { return TTOperator(_t); });
 
     // ------------------------------------------------------------------ generic TensorNetwork path of <x,y>
     // (contraction order of the reference's heuristics on the 2d+4-node network; host-only planning)
