@@ -8,6 +8,7 @@
 #include "xerus/tensor.h"
 #include "xerus/tensorNetwork.h"
 #include "xerus/ttNetwork.h"
+#include "xerus/algorithms/als.h"
 
 namespace xerus {
 namespace gpu {

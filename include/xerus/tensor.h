@@ -174,6 +174,11 @@ Tensor operator/(Tensor _tensor, const value_t _divisor);
 
 inline value_t frob_norm(const Tensor& _tensor) { return _tensor.frob_norm(); }
 
+/// A X = B with the first B.degree() - extraDegree modes of A contracted against B (tensor.cpp:1654-1704);
+/// dispatch of blasWrapper::solve (blasLapackWrapper.cpp:540-640)
+void solve(Tensor& _X, const Tensor& _A, const Tensor& _B, const size_t _extraDegree = 0);
+/// minimum-norm least-squares solution (tensor.cpp:1583-1651, dgelsd semantics)
+void solve_least_squares(Tensor& _X, const Tensor& _A, const Tensor& _B, const size_t _extraDegree = 0);
 void calculate_svd(Tensor& _U, Tensor& _S, Tensor& _Vt, Tensor _input, const size_t _splitPos, const size_t _maxRank,
                    const value_t _eps);
 void calculate_qr(Tensor& _Q, Tensor& _R, Tensor _input, const size_t _splitPos);

@@ -126,6 +126,14 @@ int xrs_rq(xrs_handle_t handle, double* R, double* Q, const double* A, size_t m,
 /** Thin SVD A = U*diag(S)*Vt, U: m x k, S: k, Vt: k x n, k = min(m,n), S descending
  *  (replaces blasWrapper::svd / dgesdd 'S', blasLapackWrapper.cpp:201-232). */
 int xrs_svd(xrs_handle_t handle, double* U, double* S, double* Vt, const double* A, size_t m, size_t n);
+/** Solve A X = B, A m x n, B m x p, X n x p (replaces blasWrapper::solve, blasLapackWrapper.cpp:540-640):
+ *  the reference's dispatch (m != n: least squares; not symmetric: general; symmetric with a positive
+ *  diagonal: Cholesky, falling back to the general path). Cholesky is blocked (any n); the general and
+ *  least-squares paths are the SVD solve of xrs_solve_least_squares (min(m, n) <= 512). Synchronises. */
+int xrs_solve(xrs_handle_t handle, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
+/** Minimum-norm least-squares solution of A X = B (replaces blasWrapper::solve_least_squares / dgelsd,
+ *  blasLapackWrapper.cpp:647-721): X = V S^+ U^T B, singular values <= EPSILON * sigma_max dropped. */
+int xrs_solve_least_squares(xrs_handle_t handle, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
 /** Singular values and right singular vectors of the rows of A (p x q, p <= q <= 512) by one-sided
  *  Jacobi -- the SVD step of the truncating TT round (TTNetwork::round's per-edge svd,
  *  ttNetwork.cpp:644-665, without U). S: p descending; Vt: p x q, orthonormal rows for S > 0.

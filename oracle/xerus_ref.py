@@ -449,3 +449,161 @@ def op_op_cores(A: Sequence[np.ndarray], B: Sequence[np.ndarray]) -> List[np.nda
         C = np.einsum('aijd,bjkc->abikdc', Ak, Bk)
         out.append(np.ascontiguousarray(C.reshape(ra * rb, n, p, ra2 * rb2)))
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# ALS (src/xerus/algorithms/als.cpp:35-565), single site, dense local solves (numpy).
+def als(A: Sequence[np.ndarray] | None, x: TT, b: TT, spd: bool = True, num_half_sweeps: int = 0, eps: float = 1e-6,
+        asd: bool = False, use_residual: bool = False, preserve_core: bool = True) -> float:
+    """ALSVariant::solve restated for one site: x is modified in place, the last energy is returned.
+    A: operator cores (r, n, m, r') or None (approximate b). Local operators: x A x (spd) or x A^T A x."""
+    d = x.order
+    canon_end, core_end = x.canonicalized, x.core_position
+    plain = spd or A is None
+    # prepare_x_for_als (:109-187)
+    first, prod = 0, 1
+    while first + 1 < d:
+        n = x.dims[first]
+        if x.ranks[first] < prod * n:
+            break
+        cur = x.cores[first].reshape(-1, x.cores[first].shape[2])
+        x.cores[first + 1] = np.einsum('ac,cnb->anb', cur, x.cores[first + 1])
+        I = np.zeros((prod, n, prod * n))
+        for i0 in range(prod):
+            for i1 in range(n):
+                I[i0, i1, i0 * n + i1] = 1.0
+        x.cores[first] = I
+        x.canonicalized = False   # two set_component calls (ttNetwork.cpp:491): never both at the core
+        first, prod = first + 1, prod * n
+    first_not, prod = d, 1
+    while first_not > first + 1:
+        n = x.dims[first_not - 1]
+        if x.ranks[first_not - 2] < prod * n:
+            break
+        cur = x.cores[first_not - 1].reshape(x.cores[first_not - 1].shape[0], -1)
+        x.cores[first_not - 2] = np.einsum('anc,cb->anb', x.cores[first_not - 2], cur)
+        I = np.zeros((prod * n, n, prod))
+        for i1 in range(n):
+            for i2 in range(prod):
+                I[i1 * prod + i2, i1, i2] = 1.0
+        x.cores[first_not - 1] = I
+        x.canonicalized = False
+        first_not, prod = first_not - 1, prod * n
+    if canon_end and core_end < first:
+        x.canonicalized, x.core_position = True, first
+    else:
+        if canon_end and core_end >= first_not:
+            x.canonicalized, x.core_position = True, first_not - 1
+        x.move_core(first, keep_rank=True)
+
+    def op_left(E, k):
+        X, Ak = x.cores[k], A[k]
+        if spd:
+            return np.einsum('pqr,pnc,qnmd,rme->cde', E, X, Ak, X)
+        return np.einsum('pqrs,pnc,qmnd,rmle,slf->cdef', E, X, Ak, Ak, X)
+
+    def op_right(E, k):
+        X, Ak = x.cores[k], A[k]
+        if spd:
+            return np.einsum('pnc,qnmd,rme,cde->pqr', X, Ak, X, E)
+        return np.einsum('pnc,qmnd,rmle,slf,cdef->pqrs', X, Ak, Ak, X, E)
+
+    def rhs_left(E, k):
+        X, B = x.cores[k], b.cores[k]
+        if plain:
+            return np.einsum('pq,pnc,qnd->cd', E, B, X)
+        return np.einsum('pqr,pnc,qnmd,rme->cde', E, B, A[k], X)
+
+    def rhs_right(E, k):
+        X, B = x.cores[k], b.cores[k]
+        if plain:
+            return np.einsum('pnc,qnd,cd->pq', B, X, E)
+        return np.einsum('pnc,qnmd,rme,cde->pqr', B, A[k], X, E)
+
+    one_op = np.ones((1, 1, 1)) if plain else np.ones((1, 1, 1, 1))
+    one_rhs = np.ones((1, 1)) if plain else np.ones((1, 1, 1))
+    oL, oR, bL, bR = [one_op], [one_op], [one_rhs], [one_rhs]
+    for i in range(d - 1, first, -1):
+        if A is not None:
+            oR.append(op_right(oR[-1], i))
+        bR.append(rhs_right(bR[-1], i))
+    for i in range(first):
+        if A is not None:
+            oL.append(op_left(oL[-1], i))
+        bL.append(rhs_left(bL[-1], i))
+    normB = b.frob_norm() if b.canonicalized else float(np.linalg.norm(b.full()))
+    cur = first
+
+    def residual():
+        if A is None:
+            return float(np.linalg.norm(x.full() - b.full()))
+        if spd:
+            Ax = TT(op_apply_cores(A, x.cores)).full()
+            return float(np.linalg.norm(Ax - b.full())) / normB
+        X, Ak, B = x.cores[cur], A[cur], b.cores[cur]
+        xAtAx = np.einsum('pqrs,pnc,qmnd,rmle,slf,cdef->', oL[-1], X, Ak, Ak, X, oR[-1])
+        bAx = np.einsum('pqr,pnc,qnmd,rme,cde->', bL[-1], B, Ak, X, bR[-1])
+        return float(np.sqrt(xAtAx - 2 * bAx + normB ** 2) / normB)
+
+    def energy():
+        if use_residual or (A is not None and not spd):
+            return residual()
+        X, B = x.cores[cur], b.cores[cur]
+        bx = np.einsum('pq,pnc,qnd,cd->', bL[-1], B, X, bR[-1])
+        if A is None:
+            return float(0.5 * np.sum(X * X) - bx)
+        xAx = np.einsum('pqr,pnc,qnmd,rme,cde->', oL[-1], X, A[cur], X, oR[-1])
+        return float(abs(0.5 * xAx - bx))
+
+    last2, last, en = 1e102, 1e101, energy()
+    half, increasing = 0, True
+    while True:
+        if A is not None:
+            Ak = A[cur]
+            if spd:
+                Aloc = np.einsum('arp,rijs,bsc->aibpjc', oL[-1], Ak, oR[-1])
+                rhs = np.einsum('ra,ric,cb->aib', bL[-1], b.cores[cur], bR[-1])
+            else:
+                Aloc = np.einsum('aqrp,qyis,ryjt,bstc->aibpjc', oL[-1], Ak, Ak, oR[-1])
+                rhs = np.einsum('rqa,ric,qijd,cdb->ajb', bL[-1], b.cores[cur], Ak, bR[-1])
+            shp = x.cores[cur].shape
+            N = int(np.prod(shp))
+            M = Aloc.reshape(N, N)
+            if asd:
+                xv = x.cores[cur].reshape(N)
+                grad = rhs.reshape(N) - M @ xv
+                if spd:
+                    alpha = float(grad @ grad) / float(grad @ (M @ grad))
+                else:
+                    grad = M.T @ grad
+                    alpha = float(np.linalg.norm(grad)) / float(np.linalg.norm(M @ grad))
+                x.cores[cur] = (xv + alpha * grad).reshape(shp)
+            else:
+                x.cores[cur] = np.linalg.solve(M, rhs.reshape(N)).reshape(shp)
+        else:
+            x.cores[cur] = np.einsum('ra,ric,cb->aib', bL[-1], b.cores[cur], bR[-1])
+        at_end = (not increasing and cur == first) or (increasing and cur == first_not - 1)
+        if at_end:
+            half += 1
+            last2, last, en = last, en, energy()
+            if half == num_half_sweeps or abs(last - en) < eps or abs(last2 - en) < eps or first_not - first <= 1:
+                if canon_end and preserve_core:
+                    x.move_core(core_end, keep_rank=True)
+                return en
+            increasing = not increasing
+        if increasing:
+            x.move_core(cur + 1, keep_rank=True)
+            if A is not None:
+                oR.pop()
+                oL.append(op_left(oL[-1], cur))
+            bR.pop()
+            bL.append(rhs_left(bL[-1], cur))
+            cur += 1
+        else:
+            x.move_core(cur - 1, keep_rank=True)
+            if A is not None:
+                oL.pop()
+                oR.append(op_right(oR[-1], cur))
+            bL.pop()
+            bR.append(rhs_right(bR[-1], cur))
+            cur -= 1

@@ -144,8 +144,16 @@ def test_operator_tt_svd_and_round(xe, ref):
     o = ref.tt_svd(inter, 1e-6, [0, 0])
     assert A.ranks() == o.ranks == [2, 3]
     assert _rel(xe.Tensor(A).to_ndarray(), Af) <= 1e-8
+    # a canonical sum is re-canonicalised with the rank-revealing QC (ttNetwork.cpp:841-843): 2A has A's ranks
     S = A + A
-    assert S.ranks() == [4, 6]
-    S.round(1e-12)
     assert S.ranks() == [2, 3]
     assert _rel(xe.Tensor(S).to_ndarray(), 2 * Af) <= 1e-8
+    # a non-canonical summand keeps the block-diagonal ranks; round() then cuts them
+    B = xe.TTOperator(A)
+    B.set_component(1, B.get_component(1))   # set_component away from the core drops canonicalized (:491)
+    assert not B.canonicalized
+    S2 = B + A
+    assert S2.ranks() == [4, 6]
+    S2.round(1e-12)
+    assert S2.ranks() == [2, 3]
+    assert _rel(xe.Tensor(S2).to_ndarray(), 2 * Af) <= 1e-8

@@ -50,6 +50,8 @@ SIGNATURES = {
     "xrs_qr": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
     "xrs_rq": (C.c_int, [_DP, _DP, _DP, _DP, _SZ, _SZ]),
     "xrs_svd": (C.c_int, [_DP, _DP, _DP, _DP, _DP, _SZ, _SZ]),
+    "xrs_solve": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ, _DP, _SZ]),
+    "xrs_solve_least_squares": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ, _DP, _SZ]),
     "xrs_svd_rows_vt": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ, C.c_int]),
     "xrs_tt_operator_apply": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                         C.POINTER(_SZ), C.POINTER(_DP), C.c_int, C.POINTER(_DP)]),
@@ -264,6 +266,15 @@ class Handle:
         U, S, Vt = self.empty((m, k)), self.empty((k,)), self.empty((k, n))
         _check("xrs_svd", self.lib.xrs_svd(self.h, _DP(U.ptr), _DP(S.ptr), _DP(Vt.ptr), _DP(A.ptr), m, n))
         return U, S, Vt
+
+    def solve(self, A: "DeviceArray", B: "DeviceArray", least_squares: bool = False):
+        """X with A X = B (xrs_solve; least_squares: xrs_solve_least_squares). B: m x p (or length m)."""
+        m, n = A.shape
+        p = B.shape[1] if len(B.shape) == 2 else 1
+        X = self.empty((n, p) if len(B.shape) == 2 else (n,))
+        fn = "xrs_solve_least_squares" if least_squares else "xrs_solve"
+        _check(fn, getattr(self.lib, fn)(self.h, _DP(X.ptr), _DP(A.ptr), m, n, _DP(B.ptr), p))
+        return X
 
     def svd_rows_vt(self, A: "DeviceArray", kernel: int = 0):
         """(S, Vt, sweeps) of the rows of A (p <= q <= 512) by one-sided Jacobi (xrs_svd_rows_vt)."""

@@ -620,6 +620,41 @@ static Tensor::DimensionTuple dims_with(const Tensor::DimensionTuple& d, size_t 
 }
 
 // tensor.cpp:1424-1489
+namespace {
+// shared shape logic of solve / solve_least_squares (tensor.cpp:1585-1606, 1659-1681)
+void solve_impl(Tensor& _X, const Tensor& _A, const Tensor& _B, const size_t _extraDegree, bool _ls) {
+    XERUS_REQUIRE(&_X != &_B && &_X != &_A, "Not supportet yet");
+    XERUS_REQUIRE(_B.degree() >= _extraDegree, "Inconsistent dimensions.");
+    const size_t degM = _B.degree() - _extraDegree;
+    XERUS_REQUIRE(_A.degree() >= degM, "Inconsistent dimensions.");
+    const size_t degN = _A.degree() - degM;
+    for (size_t i = 0; i < degM; ++i) XERUS_REQUIRE(_A.dimensions[i] == _B.dimensions[i], "Inconsistent dimensions.");
+    Tensor::DimensionTuple newDimX(_A.dimensions.begin() + long(degM), _A.dimensions.end());
+    newDimX.insert(newDimX.end(), _B.dimensions.begin() + long(degM), _B.dimensions.end());
+    size_t m = 1, n = 1, p = 1;
+    for (size_t i = 0; i < degM; ++i) m *= _A.dimensions[i];
+    for (size_t i = degM; i < degM + degN; ++i) n *= _A.dimensions[i];
+    for (size_t i = degM; i < _B.degree(); ++i) p *= _B.dimensions[i];
+    Tensor X(newDimX, Tensor::Representation::Dense, Tensor::Initialisation::None);
+    xrs_handle_t h = gpu::handle();
+    const double* Ad = _A.device_data();
+    const double* Bd = _B.device_data();
+    double* Xd = X.device_data_for_write();
+    guard([&] {
+        if (_ls) xrs::svd_solve(h, Xd, Ad, m, n, Bd, p);
+        else xrs::solve_dense(h, Xd, Ad, m, n, Bd, p);
+    });
+    X.factor = _B.factor / _A.factor;   // (:1703)
+    _X = std::move(X);
+}
+}  // namespace
+
+void solve(Tensor& _X, const Tensor& _A, const Tensor& _B, const size_t _extraDegree) { solve_impl(_X, _A, _B, _extraDegree, false); }
+
+void solve_least_squares(Tensor& _X, const Tensor& _A, const Tensor& _B, const size_t _extraDegree) {
+    solve_impl(_X, _A, _B, _extraDegree, true);
+}
+
 void calculate_svd(Tensor& _U, Tensor& _S, Tensor& _Vt, Tensor _input, const size_t _splitPos, const size_t _maxRank,
                    const value_t _eps) {
     XERUS_REQUIRE(0 <= _eps && _eps < 1, "Epsilon must be fullfill 0 <= _eps < 1.");

@@ -142,6 +142,7 @@ void TTTensor::set_component(const size_t _idx, Tensor _T) {
     XERUS_REQUIRE(_T.degree() == 3, "Component " << _idx << " must have degree 3. Given: " << _T.degree());
     dimensions[_idx] = _T.dimensions[1];
     components[_idx] = std::move(_T);
+    canonicalized = canonicalized && corePosition == _idx;   // ttNetwork.cpp:491
 }
 
 bool TTTensor::exceeds_maximal_ranks() const {
@@ -237,8 +238,8 @@ TTTensor& TTTensor::operator*=(const value_t _factor) {
 
 TTTensor& TTTensor::operator/=(const value_t _divisor) { return *this *= 1 / _divisor; }
 
-// block-diagonal cores (ttNetwork.cpp:797-847). Unlike the reference, which keeps its `canonicalized`
-// flag (and thus a stale core norm) after the sum, a canonical TT is re-orthogonalised to its core.
+// block-diagonal cores (ttNetwork.cpp:797-847); a canonical TT is re-canonicalised to its core position
+// (move_core with the rank-revealing QC, :841-843), which may cut the summed ranks
 TTTensor& TTTensor::operator+=(const TTTensor& _other) {
     XERUS_REQUIRE(dimensions == _other.dimensions, "The dimensions in TT sum must coincide.");
     require_correct_format();

@@ -282,6 +282,40 @@ PYBIND11_MODULE(xerus, m) {
         .def("__copy__", [](const TTTensor& _t) { return TTTensor(_t); });
     m.def("dot", [](const TTTensor& _x, const TTTensor& _y) { return dot(_x, _y); });
 
+    // ------------------------------------------------------------------ ALS (algorithms/als.h)
+    py::class_<ALSVariant>(m, "ALSVariant")
+        .def_readwrite("sites", &ALSVariant::sites)
+        .def_readwrite("numHalfSweeps", &ALSVariant::numHalfSweeps)
+        .def_readwrite("convergenceEpsilon", &ALSVariant::convergenceEpsilon)
+        .def_readwrite("useResidualForEndCriterion", &ALSVariant::useResidualForEndCriterion)
+        .def_readwrite("preserveCorePosition", &ALSVariant::preserveCorePosition)
+        .def_readwrite("assumeSPD", &ALSVariant::assumeSPD)
+        .def("__call__", [](const ALSVariant& _s, const TTOperator& _A, TTTensor& _x, const TTTensor& _b, value_t _eps) {
+            return _s(_A, _x, _b, _eps);
+        })
+        .def("__call__", [](const ALSVariant& _s, const TTOperator& _A, TTTensor& _x, const TTTensor& _b, size_t _n) {
+            return _s(_A, _x, _b, _n);
+        })
+        .def("__call__", [](const ALSVariant& _s, const TTOperator& _A, TTTensor& _x, const TTTensor& _b) { return _s(_A, _x, _b); })
+        .def("__call__", [](const ALSVariant& _s, TTTensor& _x, const TTTensor& _b, value_t _eps) { return _s(_x, _b, _eps); })
+        .def("__call__", [](const ALSVariant& _s, TTTensor& _x, const TTTensor& _b, size_t _n) { return _s(_x, _b, _n); })
+        .def("__call__", [](const ALSVariant& _s, TTTensor& _x, const TTTensor& _b) { return _s(_x, _b); })
+        .def("__copy__", [](const ALSVariant& _s) { return ALSVariant(_s); });
+    m.attr("ALS") = py::cast(ALSVariant(ALS));
+    m.attr("ALS_SPD") = py::cast(ALSVariant(ALS_SPD));
+    m.attr("ASD") = py::cast(ALSVariant(ASD));
+    m.attr("ASD_SPD") = py::cast(ALSVariant(ASD_SPD));
+    m.def("solve", [](const Tensor& _A, const Tensor& _B, size_t _extra) {
+        Tensor X;
+        solve(X, _A, _B, _extra);
+        return X;
+    }, py::arg("A"), py::arg("B"), py::arg("extraDegree") = 0);
+    m.def("solve_least_squares", [](const Tensor& _A, const Tensor& _B, size_t _extra) {
+        Tensor X;
+        solve_least_squares(X, _A, _B, _extra);
+        return X;
+    }, py::arg("A"), py::arg("B"), py::arg("extraDegree") = 0);
+
     // ------------------------------------------------------------------ TTOperator (TTNetwork<true>)
     py::class_<TTOperator>(m, "TTOperator")
         .def(py::init<>())

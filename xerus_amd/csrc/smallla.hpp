@@ -1,5 +1,7 @@
 // Launch wrappers of the small dense kernels (smallla.hip) and the factorisation drivers (linalg.cpp).
 #pragma once
+#include <vector>
+
 #include "elementwise.hpp"
 
 namespace xrs {
@@ -80,6 +82,13 @@ size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double
 void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* R);
 void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* Q);
 void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt);
+
+// dense solves (solve.hip): blasWrapper::solve / solve_least_squares semantics; chol_blocked / chol_solve:
+// SPD factorisation of any size (L lower, Z the diagonal-block inverses) and the two triangular sweeps
+void solve_dense(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
+void svd_solve(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
+bool chol_blocked(xrs_handle_t h, const double* A, size_t n, double* L, std::vector<DevBuf>& Z);
+void chol_solve(xrs_handle_t h, const double* L, const std::vector<DevBuf>& Z, size_t n, const double* B, size_t p, double* X);
 
 // helpers
 void transpose(xrs_handle_t h, double* out, const double* in, size_t rows, size_t cols);

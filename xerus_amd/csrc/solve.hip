@@ -1,0 +1,200 @@
+// Dense linear solves (blasWrapper::solve / solve_least_squares, blasLapackWrapper.cpp:540-721) and the
+// blocked Cholesky they use for symmetric positive definite systems of any size.
+//
+// Dispatch as the reference's (mldivide order, :547-640): m != n -> least squares; not symmetric ->
+// general solve; symmetric with a positive diagonal -> Cholesky, and if that fails the general path.
+// The reference's LU (dgesv), LDL^T (dsysv) and dgelsd all return the solution of a nonsingular system
+// (dgelsd: the minimum-norm least-squares solution, singular values <= EPSILON sigma_max dropped); here
+// the general and least-squares paths are one SVD solve x = V S^+ U^T b with that same cut (min(m, n)
+// <= 512), and the Cholesky path is a right-looking blocked factorisation: 256-column diagonal blocks by
+// the register-resident potrf + explicit triangular inverse, panels and trailing updates as MFMA GEMMs
+// (n unbounded). Triangular solves use the diagonal-block inverses, so both sweeps are GEMMs too.
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "smallla.hpp"
+
+namespace xrs {
+namespace {
+
+constexpr double kEps = 2.220446049250313e-16;
+constexpr int kCholBlock = 256;
+
+// dst (rows x cols, ld ldd) = alpha * src (ld lds)
+__global__ void __launch_bounds__(256) k_copy2d(double* __restrict__ dst, size_t ldd, const double* __restrict__ src, size_t lds,
+                                                size_t rows, size_t cols, double alpha) {
+    const size_t total = rows * cols;
+    for (size_t e = size_t(blockIdx.x) * 256 + threadIdx.x; e < total; e += size_t(gridDim.x) * 256) {
+        const size_t r = e / cols, c = e - r * cols;
+        dst[r * ldd + c] = alpha * src[r * lds + c];
+    }
+}
+
+void copy2d(xrs_handle_t h, double* dst, size_t ldd, const double* src, size_t lds, size_t rows, size_t cols, double alpha = 1.0) {
+    if (!rows || !cols) return;
+    const size_t blocks = std::min<size_t>((rows * cols + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_copy2d, dim3(unsigned(blocks)), dim3(256), 0, h->stream, dst, ldd, src, lds, rows, cols, alpha);
+    check_launch("k_copy2d");
+}
+
+// per-block partial maxima of A (signed values, as the reference's is_symmetric, :501-505)
+__global__ void __launch_bounds__(256) k_max_partial(const double* __restrict__ A, size_t total, double* __restrict__ part) {
+    double m = 0.0;
+    for (size_t e = size_t(blockIdx.x) * 256 + threadIdx.x; e < total; e += size_t(gridDim.x) * 256) m = fmax(m, A[e]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
+// flags[0] = 1 if some |A_ij - A_ji| >= 4 max eps (not symmetric, :507-513); flags[1] = 1 if the
+// diagonal is not positive definite-looking (A_00 > 0 and A_ii >= eps, :519-528)
+__global__ void __launch_bounds__(256) k_sym_flags(const double* __restrict__ A, size_t n, const double* __restrict__ part, int nparts,
+                                                   int* __restrict__ flags) {
+    double mx = 0.0;
+    for (int i = 0; i < nparts; ++i) mx = fmax(mx, part[i]);
+    const double thr = 4.0 * mx * kEps;
+    bool asym = false, baddiag = false;
+    for (size_t e = size_t(blockIdx.x) * 256 + threadIdx.x; e < n * n; e += size_t(gridDim.x) * 256) {
+        const size_t i = e / n, j = e - i * n;
+        if (j > i && fabs(A[i * n + j] - A[j * n + i]) >= thr) asym = true;
+        if (i == j && (i == 0 ? !(A[0] > 0.0) : A[e] < kEps)) baddiag = true;
+    }
+    if (asym) __hip_atomic_fetch_or(&flags[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (baddiag) __hip_atomic_fetch_or(&flags[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sinv[i] = 1 / S[i] for S[i] > rcond * S[0], else 0 (dgelsd's rank cut)
+__global__ void k_inv_cut(const double* __restrict__ S, int k, double rcond, double* __restrict__ sinv) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < k) sinv[i] = (S[i] > rcond * S[0]) ? 1.0 / S[i] : 0.0;
+}
+
+}  // namespace
+
+// A = L L^T for symmetric positive definite A (n x n); L lower (n x n, upper part zero), Z the explicit
+// inverses of the diagonal blocks (kCholBlock x kCholBlock each, packed). Returns false if a diagonal
+// block is not positive definite (synchronises once).
+bool chol_blocked(xrs_handle_t h, const double* A, size_t n, double* L, std::vector<DevBuf>& Z) {
+    const size_t nblk = (n + kCholBlock - 1) / kCholBlock;
+    DevBuf W(h, n * n * 8), st(h, nblk * 4), D(h, size_t(kCholBlock) * kCholBlock * 8), Dinv(h, dinv_elems(kCholBlock) * 8);
+    DevBuf P(h, n * kCholBlock * 8), T(h, n * n * 8);
+    XRS_HIP(hipMemcpyAsync(W.d(), A, n * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    XRS_HIP(hipMemsetAsync(L, 0, n * n * 8, h->stream));
+    Z.clear();
+    for (size_t jb = 0; jb < nblk; ++jb) {
+        const size_t j0 = jb * kCholBlock, b = std::min<size_t>(kCholBlock, n - j0), rest = n - j0 - b;
+        copy2d(h, D.d(), b, W.d() + j0 * n + j0, n, b, b);
+        potrf(h, D.d(), int(b), 0.0, Dinv.d(), st.as<int>() + jb);
+        Z.emplace_back(h, b * b * 8);
+        TrinvBatch tb{};
+        tb.L[0] = D.d();
+        tb.Dinv[0] = Dinv.d();
+        tb.X[0] = Z.back().d();
+        tb.n[0] = int(b);
+        trinv_batched(h, tb, 1);
+        copy2d(h, L + j0 * n + j0, n, D.d(), b, b, b);
+        if (!rest) break;
+        // panel L_ij = W_ij Z_jj^T, trailing W -= L_ij L_ij^T
+        gemm(h, P.d(), rest, b, 1.0, W.d() + (j0 + b) * n + j0, n, false, b, Z.back().d(), b, true);
+        copy2d(h, L + (j0 + b) * n + j0, n, P.d(), b, rest, b);
+        gemm_sym(h, T.d(), rest, 1.0, P.d(), b, false, b, P.d(), b, true);
+        const size_t od[2] = {n, n}, id[2] = {rest, rest}, off[2] = {j0 + b, j0 + b};
+        offset_add(h, W.d(), od, T.d(), id, 2, off, -1.0);
+    }
+    std::vector<int> s(nblk);
+    read_status(h, st.as<int>(), int(nblk), s.data());
+    for (int v : s)
+        if (v != 0) return false;
+    return true;
+}
+
+// X (n x p) = (L L^T)^{-1} B with the factors of chol_blocked
+void chol_solve(xrs_handle_t h, const double* L, const std::vector<DevBuf>& Z, size_t n, const double* B, size_t p, double* X) {
+    const size_t nblk = Z.size();
+    DevBuf Y(h, n * p * 8), R(h, size_t(kCholBlock) * p * 8), T(h, size_t(kCholBlock) * p * 8);
+    for (size_t jb = 0; jb < nblk; ++jb) {   // L Y = B
+        const size_t j0 = jb * kCholBlock, b = std::min<size_t>(kCholBlock, n - j0);
+        XRS_HIP(hipMemcpyAsync(R.d(), B + j0 * p, b * p * 8, hipMemcpyDeviceToDevice, h->stream));
+        if (j0) {
+            gemm(h, T.d(), b, p, 1.0, L + j0 * n, n, false, j0, Y.d(), p, false);
+            axpy(h, R.d(), -1.0, T.d(), b * p);
+        }
+        gemm(h, Y.d() + j0 * p, b, p, 1.0, Z[jb].d(), b, false, b, R.d(), p, false);
+    }
+    for (size_t jb = nblk; jb-- > 0;) {   // L^T X = Y
+        const size_t j0 = jb * kCholBlock, b = std::min<size_t>(kCholBlock, n - j0), rest = n - j0 - b;
+        XRS_HIP(hipMemcpyAsync(R.d(), Y.d() + j0 * p, b * p * 8, hipMemcpyDeviceToDevice, h->stream));
+        if (rest) {
+            gemm(h, T.d(), b, p, 1.0, L + (j0 + b) * n + j0, n, true, rest, X + (j0 + b) * p, p, false);
+            axpy(h, R.d(), -1.0, T.d(), b * p);
+        }
+        gemm(h, X + j0 * p, b, p, 1.0, Z[jb].d(), b, true, b, R.d(), p, false);
+    }
+}
+
+// x = V S^+ U^T b, singular values <= EPSILON sigma_0 dropped (dgelsd with rcond = xerus::EPSILON, :704)
+void svd_solve(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p) {
+    const size_t k = std::min(m, n);
+    XRS_REQUIRE(k <= size_t(kSmallMax), "solve: the general / least-squares path needs min(m, n) <= 512");
+    DevBuf U(h, m * k * 8), S(h, k * 8), Vt(h, k * n * 8), Si(h, k * 8), T(h, k * p * 8);
+    svd(h, A, m, n, U.d(), S.d(), Vt.d());
+    hipLaunchKernelGGL(k_inv_cut, dim3(unsigned((k + 255) / 256)), dim3(256), 0, h->stream, S.d(), int(k), 8.0 * kEps, Si.d());
+    check_launch("k_inv_cut");
+    gemm(h, T.d(), k, p, 1.0, U.d(), k, true, m, B, p, false);   // U^T B
+    scale_rows(h, T.d(), Si.d(), k, p);
+    gemm(h, X, n, p, 1.0, Vt.d(), n, true, k, T.d(), p, false);   // V (S^+ U^T B)
+}
+
+void solve_dense(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p) {
+    if (m != n) {
+        svd_solve(h, X, A, m, n, B, p);
+        return;
+    }
+    const size_t total = n * n;
+    const int nparts = int(std::min<size_t>((total + 255) / 256, 1024));
+    DevBuf part(h, size_t(nparts) * 8), flags(h, 64);
+    XRS_HIP(hipMemsetAsync(flags.d(), 0, 64, h->stream));
+    hipLaunchKernelGGL(k_max_partial, dim3(unsigned(nparts)), dim3(256), 0, h->stream, A, total, part.d());
+    check_launch("k_max_partial");
+    hipLaunchKernelGGL(k_sym_flags, dim3(unsigned(nparts)), dim3(256), 0, h->stream, A, n, part.d(), nparts, flags.as<int>());
+    check_launch("k_sym_flags");
+    int fl[2] = {0, 0};
+    read_status(h, flags.as<int>(), 2, fl);
+    if (!fl[0] && !fl[1]) {
+        DevBuf L(h, n * n * 8);
+        std::vector<DevBuf> Z;
+        if (chol_blocked(h, A, n, L.d(), Z)) {
+            chol_solve(h, L.d(), Z, n, B, p, X);
+            return;
+        }
+    }
+    svd_solve(h, X, A, m, n, B, p);
+}
+
+}  // namespace xrs
+
+using namespace xrs;
+
+extern "C" {
+
+int xrs_solve(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p) {
+    return guarded([&] {
+        XRS_REQUIRE(h && X && A && B, "null argument");
+        XRS_REQUIRE(m > 0 && n > 0 && p > 0, "solve: empty system");
+        solve_dense(h, X, A, m, n, B, p);
+    });
+}
+
+int xrs_solve_least_squares(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p) {
+    return guarded([&] {
+        XRS_REQUIRE(h && X && A && B, "null argument");
+        XRS_REQUIRE(m > 0 && n > 0 && p > 0, "solve_least_squares: empty system");
+        svd_solve(h, X, A, m, n, B, p);
+    });
+}
+
+}  // extern "C"
