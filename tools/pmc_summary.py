@@ -1,9 +1,10 @@
 """Summarise the PMC passes of tools/pmc_bench.sh per kernel family and write profiles/<tag>/pmc_*.
 
-HBM traffic per k_gemm_f64 launch = FETCH_SIZE + WRITE_SIZE (rocprofv3 derived counters, KiB). Per
-MI355X_MICROARCH.md (HBM section) FETCH_SIZE reads exactly half of a 16-B/lane streaming read on gfx950;
-the GEMM's global loads are 8-B/lane, for which the guide gives no calibration, so the raw value is
-reported with that caveat. Usage: python tools/pmc_summary.py gpurun_out/pmc profiles/r01
+HBM traffic per k_gemm_f64 launch = 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 derived counters, KiB).
+MI355X_MICROARCH.md (HBM section): FETCH_SIZE reads exactly half of a 16-B/lane streaming read on gfx950;
+the 8-B/lane loads and stores of our kernels are calibrated by tools/fetch_calib.hip (pass "calf"/"calw"
+in the source directory): the factors measured there (FETCH x2 for 8-B and 16-B loads, WRITE x1 for 8-B
+stores) are applied when present. Usage: python tools/pmc_summary.py gpurun_out/pmc2 profiles/r02
 """
 import collections
 import csv
@@ -26,6 +27,19 @@ def load(pass_name):
     return per
 
 
+# calibration: known byte counts of tools/fetch_calib.hip
+cal = {"fetch": None, "write": None}
+for name, known in (("calf", {"k_read8": 1 << 30, "k_read16": 1 << 30}), ("calw", {"k_write8": 1 << 28})):
+    for fam, counters in load(name).items():
+        key = fam.split("(")[0]
+        for c, v in counters.items():
+            if key in known and known[key]:
+                factor = known[key] / (sum(v) / len(v) * 1024)
+                cal.setdefault("factors", {})[f"{key}:{c}"] = factor
+if "factors" in cal:
+    cal["fetch"] = cal["factors"].get("k_read8:FETCH_SIZE")
+    cal["write"] = cal["factors"].get("k_write8:WRITE_SIZE")
+
 summary = {}
 for p in ("fetch", "write", "mfma"):
     for fam, counters in load(p).items():
@@ -35,15 +49,20 @@ with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
     json.dump(summary, f, indent=1, sort_keys=True)
 g = summary.get("xrs::k_gemm_f64", {})
 if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
-    fetch, write = g["FETCH_SIZE"]["mean"] * 1024, g["WRITE_SIZE"]["mean"] * 1024
+    ff = cal["fetch"] or 1.0
+    wf = cal["write"] or 1.0
+    fetch, write = g["FETCH_SIZE"]["mean"] * 1024 * ff, g["WRITE_SIZE"]["mean"] * 1024 * wf
     out = {
         "hbm_bytes_per_launch": fetch + write,
         "fetch_bytes_per_launch": fetch,
         "write_bytes_per_launch": write,
+        "fetch_size_raw_kib": g["FETCH_SIZE"]["mean"],
+        "write_size_raw_kib": g["WRITE_SIZE"]["mean"],
+        "calibration": {"fetch_factor": ff, "write_factor": wf, "measured": cal.get("factors", {})},
         "dispatches": g["FETCH_SIZE"]["dispatches"],
-        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py --steps 3 --warmup 1, "
-                  "mean per k_gemm_f64 dispatch; raw counters (gfx950 FETCH_SIZE halves 16-B/lane reads; "
-                  "these 8-B/lane loads are uncalibrated); profiles/r01/pmc_summary.json",
+        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py --no-cpu --no-cfg5 --no-extras "
+                  "--steps 3 --warmup 1, mean per k_gemm_f64 dispatch, corrected by the 8-B load/store calibration of "
+                  "tools/fetch_calib.hip (FETCH x%.3f, WRITE x%.3f); %s/pmc_summary.json" % (ff, wf, dst),
     }
     if "SQ_VALU_MFMA_BUSY_CYCLES" in g and "GRBM_GUI_ACTIVE" in g:
         out["mfma_busy_cycles_per_dispatch"] = g["SQ_VALU_MFMA_BUSY_CYCLES"]["mean"]
