@@ -593,7 +593,10 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
     const bool blocks_ok = q <= SVB_QMAX;
     XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 512");
     if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
-        if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+        // register tiling E * 32 columns: the narrowest that holds q (padding costs FMAs and LDS traffic)
+        if (q <= 64) launch_blocks<16, 32, 2, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+        else if (q <= 128) launch_blocks<16, 32, 4, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+        else if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
         else launch_blocks<16, 32, 16, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
     } else if (jacobi_vt_fits_lds(p, q)) {
         hipLaunchKernelGGL(k_jacobi_vt_lds, dim3(1), dim3(SVL_THREADS), 0, h->stream, W, ldw, int(trans), p, q, max_sweeps, S, Vt,
@@ -614,7 +617,9 @@ void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int
     XRS_REQUIRE(jacobi_usv_fits(p, q), "jacobi_usv: need p <= q and 32 ceil(q / 32) + p <= 1024");
     KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * (q + p) * 6.0, 16.0 * double(p) * (q + p));
     const int width = 32 * ((q + 31) / 32) + p;
-    if (width <= 512) launch_blocks<16, 32, 16, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
+    if (width <= 128) launch_blocks<16, 32, 4, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
+    else if (width <= 256) launch_blocks<16, 32, 8, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
+    else if (width <= 512) launch_blocks<16, 32, 16, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
     else launch_blocks<8, 32, 32, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
 }
 
