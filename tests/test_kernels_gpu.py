@@ -33,6 +33,27 @@ def test_permute_bit_exact(handle, ref, dims, shuffle):
     assert np.array_equal(out, expect)
 
 
+def test_permute_all_orders_small_modes(handle, ref):
+    """Every permutation of a 5-mode tensor with small, unequal modes (the grouped-mode transpose path:
+    groups of innermost input / output modes, ragged flattened extents), bit-exact against the oracle."""
+    import itertools
+
+    dims = (3, 5, 2, 7, 4)
+    a = np.random.default_rng(5).standard_normal(dims)
+    d = handle.array(a)
+    for shuffle in itertools.permutations(range(5)):
+        out = handle.reshuffle(d, shuffle).numpy()
+        assert np.array_equal(out, ref.reshuffle(a, shuffle)), shuffle
+
+
+@pytest.mark.parametrize("dims,shuffle", [((20, 20, 20, 20), (3, 2, 1, 0)), ((6, 40, 6, 40), (1, 3, 0, 2)),
+                                          ((9, 9, 9, 9, 9), (4, 0, 3, 1, 2)), ((2, 300, 3, 17), (3, 1, 0, 2))])
+def test_permute_grouped_shapes(handle, ref, dims, shuffle):
+    a = np.random.default_rng(6).standard_normal(dims)
+    out = handle.reshuffle(handle.array(a), shuffle).numpy()
+    assert np.array_equal(out, ref.reshuffle(a, shuffle))
+
+
 def test_permute_rejects_bad_shuffle(handle):
     from xerus_amd.capi import XrsError
 

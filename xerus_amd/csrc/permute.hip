@@ -6,7 +6,9 @@
 //   (a) the innermost mode stays innermost -> row-block copy (16-B vector loads/stores), or
 //   (b) a batched 2-D transpose between the input-contiguous mode `a` and the output-contiguous
 //       mode `b`: 32x32 fp64 tiles staged through LDS ([32][33] padding: conflict-free ds_read_b64
-//       columns), coalesced 256-B row segments on both the HBM read and the HBM write.
+//       columns), coalesced 256-B row segments on both the HBM read and the HBM write; or
+//   (c) when those modes are shorter than a tile, the same transpose between GROUPS of innermost
+//       input / output modes (flattened indices), so small modes still fill whole tiles.
 // Both are HBM-bound: algorithmic bytes = 2 * size * 8.
 #include <algorithm>
 #include <numeric>
@@ -140,12 +142,13 @@ __global__ void __launch_bounds__(256) k_permute_transpose(double* __restrict__ 
     const int tx = threadIdx.x & 31;   // fast index
     const int ty = threadIdx.x >> 5;   // 0..7
     for (size_t bi = blockIdx.y; bi < batch; bi += gridDim.y) {
-        size_t rem = bi, ioff = 0, ooff = 0;
+        unsigned rem = unsigned(bi);   // batch < 2^32 (host check)
+        size_t ioff = 0, ooff = 0;
         for (int k = a.nb - 1; k >= 0; --k) {
-            const size_t i = rem % a.bdims[k];
-            rem /= a.bdims[k];
-            ioff += i * a.bin_str[k];
-            ooff += i * a.bout_str[k];
+            const unsigned dk = unsigned(a.bdims[k]), q = rem / dk, i = rem - q * dk;
+            rem = q;
+            ioff += size_t(i) * a.bin_str[k];
+            ooff += size_t(i) * a.bout_str[k];
         }
         // read: rows along b, contiguous along a
 #pragma unroll
@@ -159,6 +162,68 @@ __global__ void __launch_bounds__(256) k_permute_transpose(double* __restrict__ 
         for (int j = 0; j < TT; j += 8) {
             const size_t ia = a0 + ty + j, ib = b0 + tx;
             if (ib < a.db && ia < a.da) out[ooff + ia * a.out_sa + ib] = tile[tx][ty + j];
+        }
+        __syncthreads();
+    }
+}
+
+// (c) the same tiled transpose between GROUPS of modes: a = the innermost input modes (contiguous in the
+// input, flattened index fa), b = the innermost output modes (contiguous in the output, index fb). Small
+// modes (the 20^6 reversal: 20 x 20 = 400) then fill whole 32 x 32 tiles instead of 20 x 20 of them.
+constexpr int kGroupMax = 4;
+struct GrArgs {
+    int na, nbm;                        // modes in the a / b groups
+    size_t adims[kGroupMax], aout[kGroupMax];   // a group, input-fastest first: extent, output stride
+    size_t bdims[kGroupMax], bin[kGroupMax];    // b group, output-fastest first: extent, input stride
+    size_t pa, pb;                      // flattened extents
+    int nbatch;
+    size_t bdim[kMaxModes], bin_str[kMaxModes], bout_str[kMaxModes];
+    unsigned tiles_a, tiles_b;
+};
+
+__global__ void __launch_bounds__(256) k_permute_grouped(double* __restrict__ out, const double* __restrict__ in, GrArgs a, size_t batch) {
+    __shared__ double tile[TT][TT + 1];
+    const unsigned t = blockIdx.x;
+    const size_t a0 = size_t(t % a.tiles_a) * TT, b0 = size_t(t / a.tiles_a) * TT;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    // per-row offsets: input offset of b rows, output offset of a rows (4 rows per thread each)
+    size_t boff[TT / 8], aoff[TT / 8];
+#pragma unroll
+    for (int j = 0; j < TT / 8; ++j) {   // 32-bit index arithmetic (flattened group extents < 2^32)
+        unsigned fb = unsigned(b0) + ty + 8 * j, fa = unsigned(a0) + ty + 8 * j;
+        size_t ob = 0, oa = 0;
+        for (int k = 0; k < a.nbm; ++k) {
+            const unsigned dk = unsigned(a.bdims[k]), q = fb / dk;
+            ob += size_t(fb - q * dk) * a.bin[k];
+            fb = q;
+        }
+        for (int k = 0; k < a.na; ++k) {
+            const unsigned dk = unsigned(a.adims[k]), q = fa / dk;
+            oa += size_t(fa - q * dk) * a.aout[k];
+            fa = q;
+        }
+        boff[j] = ob;
+        aoff[j] = oa;
+    }
+    for (size_t bi = blockIdx.y; bi < batch; bi += gridDim.y) {
+        unsigned rem = unsigned(bi);   // batch < 2^32 (host check)
+        size_t ioff = 0, ooff = 0;
+        for (int k = a.nbatch - 1; k >= 0; --k) {
+            const unsigned dk = unsigned(a.bdim[k]), q = rem / dk, i = rem - q * dk;
+            rem = q;
+            ioff += size_t(i) * a.bin_str[k];
+            ooff += size_t(i) * a.bout_str[k];
+        }
+#pragma unroll
+        for (int j = 0; j < TT / 8; ++j) {
+            const size_t fb = b0 + ty + 8 * j, fa = a0 + tx;
+            if (fb < a.pb && fa < a.pa) tile[ty + 8 * j][tx] = in[ioff + boff[j] + fa];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TT / 8; ++j) {
+            const size_t fa = a0 + ty + 8 * j, fb = b0 + tx;
+            if (fb < a.pb && fa < a.pa) out[ooff + aoff[j] + fb] = tile[tx][ty + 8 * j];
         }
         __syncthreads();
     }
@@ -195,6 +260,60 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
     XRS_REQUIRE(mb >= 0 && mb != ma, "internal: permutation plan");
     std::vector<size_t> in_str(p.n, 1);
     for (int k = p.n - 2; k >= 0; --k) in_str[k] = in_str[k + 1] * p.dims[k + 1];
+    // groups: innermost input modes (a) and innermost output modes (b) until each spans >= one tile
+    {
+        std::vector<int> out_order(p.n);   // input-mode indices, output-fastest first
+        std::iota(out_order.begin(), out_order.end(), 0);
+        std::sort(out_order.begin(), out_order.end(), [&](int x, int y) { return p.out_stride[x] < p.out_stride[y]; });
+        std::vector<char> inA(p.n, 0);
+        std::vector<int> A, B;
+        size_t pa = 1, pb = 1;
+        for (int k = p.n - 1; k >= 0 && pa < size_t(TT) && int(A.size()) < kGroupMax && k != mb; --k) {
+            A.push_back(k);
+            inA[k] = 1;
+            pa *= p.dims[k];
+        }
+        for (int r = 0; r < p.n && pb < size_t(TT) && int(B.size()) < kGroupMax && !inA[out_order[r]]; ++r) {
+            B.push_back(out_order[r]);
+            pb *= p.dims[out_order[r]];
+        }
+        if (A.size() > 1 || B.size() > 1) {
+            GrArgs g{};
+            g.na = int(A.size());
+            g.nbm = int(B.size());
+            for (int i = 0; i < g.na; ++i) {
+                g.adims[i] = p.dims[A[i]];
+                g.aout[i] = p.out_stride[A[i]];
+            }
+            for (int i = 0; i < g.nbm; ++i) {
+                g.bdims[i] = p.dims[B[i]];
+                g.bin[i] = in_str[B[i]];
+            }
+            g.pa = pa;
+            g.pb = pb;
+            std::vector<char> grouped(p.n, 0);
+            for (int k : A) grouped[k] = 1;
+            for (int k : B) grouped[k] = 1;
+            size_t batch = 1;
+            for (int k = 0; k < p.n; ++k) {
+                if (grouped[k]) continue;
+                g.bdim[g.nbatch] = p.dims[k];
+                g.bin_str[g.nbatch] = in_str[k];
+                g.bout_str[g.nbatch] = p.out_stride[k];
+                ++g.nbatch;
+                batch *= p.dims[k];
+            }
+            g.tiles_a = unsigned((pa + TT - 1) / TT);
+            g.tiles_b = unsigned((pb + TT - 1) / TT);
+            const size_t tiles = size_t(g.tiles_a) * g.tiles_b;
+            XRS_REQUIRE(tiles < (1ull << 31) && batch < (1ull << 32) && pa < (1ull << 32) && pb < (1ull << 32), "permutation too large");
+            // a few batch items per workgroup (the row offsets are computed once per workgroup)
+            const unsigned gy = unsigned(std::max<size_t>(1, std::min<size_t>({batch, 65535, (size_t(1) << 13) / tiles})));
+            hipLaunchKernelGGL(k_permute_grouped, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, out, in, g, batch);
+            check_launch("k_permute_grouped");
+            return;
+        }
+    }
     TrArgs ta{};
     ta.da = p.dims[ma];
     ta.db = p.dims[mb];
@@ -213,7 +332,7 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
     ta.tiles_a = unsigned((ta.da + TT - 1) / TT);
     ta.tiles_b = unsigned((ta.db + TT - 1) / TT);
     const size_t tiles = size_t(ta.tiles_a) * ta.tiles_b;
-    XRS_REQUIRE(tiles < (1ull << 31), "permutation too large");
+    XRS_REQUIRE(tiles < (1ull << 31) && batch < (1ull << 32), "permutation too large");
     const unsigned gy = unsigned(std::min<size_t>(batch, 65535));
     hipLaunchKernelGGL(k_permute_transpose, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, out, in, ta, batch);
     check_launch("k_permute_transpose");
