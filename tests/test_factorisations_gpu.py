@@ -72,6 +72,21 @@ def test_qr_rq(handle, m, n):
     assert np.linalg.norm(Q2h @ Q2h.T - np.eye(k)) <= TOL * k
 
 
+@pytest.mark.parametrize("m,n", [(3000, 600), (2100, 1030), (1100, 1100)])
+def test_qr_rq_above_512(handle, m, n):
+    """Orders above 512: the blocked CholeskyQR2 (chol_full, explicit inverses) -- tall QR and wide RQ."""
+    A = np.random.default_rng(m + n).standard_normal((m, n))
+    Q, R = handle.qr(handle.array(A))
+    Qh, Rh = Q.numpy(), R.numpy()
+    assert _rel(Qh @ Rh, A) <= TOL
+    assert np.abs(Qh.T @ Qh - np.eye(n)).max() <= 1e-13
+    assert np.allclose(np.tril(Rh, -1), 0.0)
+    R2, Q2 = handle.rq(handle.array(np.ascontiguousarray(A.T)))
+    R2h, Q2h = R2.numpy(), Q2.numpy()
+    assert _rel(R2h @ Q2h, A.T) <= TOL
+    assert np.abs(Q2h @ Q2h.T - np.eye(n)).max() <= 1e-13
+
+
 @pytest.mark.parametrize("m,n", [(8, 5), (5, 8), (64, 64), (128, 128), (30, 200), (200, 30), (1, 5), (5, 1),
                                  (256, 256), (512, 512), (300, 512), (512, 300), (100, 100), (90, 64)])
 def test_svd(handle, ref, m, n):

@@ -247,3 +247,38 @@ def test_round_many_edges_above_256(handle, ref):
     assert g.ranks == y.ranks == ranks
     diff, nrm = tt_diff_norm(g.cores(), x.cores)
     assert diff <= 1e-10 * nrm
+
+
+@pytest.mark.parametrize("n,ranks", [(30, [30, 600, 600, 30]), (40, [40, 1024, 40])])
+def test_round_ranks_above_512(handle, ref, n, ranks):
+    """Ranks above 512: blocked Cholesky with explicit inverses (chol_full) in the certified chain round,
+    the 8-row / 1024-column block Jacobi in the truncating round, blocked CholeskyQR2 in move_core.
+    Same tensor and exact ranks without a cut; the oracle's ranks and truncation error with one."""
+    d = len(ranks) + 1
+    x = ref.TT.random_raw([n] * d, ranks, ref.Rng(61))
+    g = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    g.round(max(ranks))
+    assert g.ranks == ranks
+    assert handle.last_round_path() == "chain"
+    gc = g.cores()
+    for c in gc[1:]:
+        M = c.reshape(c.shape[0], -1)
+        assert np.abs(M @ M.T - np.eye(M.shape[0])).max() <= 1e-12
+    diff, nrm = _tt_diff_norm(ref, gc, x.cores)
+    assert diff <= 1e-10 * nrm
+    # move the core to the end and back (QR sweeps through the > 512 unfoldings)
+    g.move_core(d - 1)
+    g.move_core(0)
+    diff, _ = _tt_diff_norm(ref, g.cores(), x.cores)
+    assert diff <= 1e-10 * nrm
+    # truncating round to half the largest rank
+    target = max(ranks) // 2
+    g2 = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    g2.round(target)
+    y = x.copy()
+    y.round(target)
+    assert g2.ranks == y.ranks
+    assert handle.last_round_path() == "truncate"
+    e_ref, _ = _tt_diff_norm(ref, y.cores, x.cores)
+    e_gpu, _ = _tt_diff_norm(ref, g2.cores(), x.cores)
+    assert abs(e_gpu - e_ref) <= 1e-6 * nrm

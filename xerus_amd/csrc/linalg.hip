@@ -148,13 +148,78 @@ static bool reference_r00_positive(xrs_handle_t h, const double* A, size_t m, si
 }
 
 // ------------------------------------------------------------------------------------------------
+// The same CholeskyQR2 (certifying downward shift) / shifted CholeskyQR3 for Gram orders above the
+// batched kernels' 512, on the blocked factorisation with explicit inverses (solve.hip chol_full): the
+// triangular solves become GEMMs with L^{-1}. No Householder last resort at this size: a matrix that
+// fails the verified shifted CholeskyQR3 (kappa >= 1/u) is rejected.
+static OrthResult orthogonalize_big(xrs_handle_t h, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL) {
+    const size_t N = wide ? m : n, M = wide ? n : m;
+    OrthResult res{false, 0.0, false};
+    const int nb = chol_full_blocks(N);
+    DevBuf G(h, N * N * 8), L1(h, N * N * 8), Z1(h, N * N * 8), L2(h, N * N * 8), Z2(h, N * N * 8), L3(h, N * N * 8),
+        Z3(h, N * N * 8), T(h, N * N * 8), Q1(h, m * n * 8), Q2(h, m * n * 8), st(h, size_t(3 * nb) * 4 + 64);
+    auto gram = [&](double* out, const double* X) {
+        if (wide) gemm_sym(h, out, N, 1.0, X, n, false, M, X, n, true);   // X X^T
+        else gemm_sym(h, out, N, 1.0, X, n, true, M, X, n, false);        // X^T X
+    };
+    auto apply = [&](const double* Z, const double* X, double* out) {   // tall: X Z^T, wide: Z X
+        if (wide) gemm(h, out, N, n, 1.0, Z, N, false, N, X, n, false);
+        else gemm(h, out, m, N, 1.0, X, n, false, N, Z, N, true);
+    };
+    auto all_zero = [&](int count) {
+        std::vector<int> s(static_cast<size_t>(count));
+        read_status(h, st.as<int>(), count, s.data());
+        for (int v : s)
+            if (v != 0) return false;
+        return true;
+    };
+    const double tau_rel = 4.0 * double(M + 2 * N) * kU;
+    gram(G.d(), A);
+    chol_full(h, G.d(), N, -tau_rel, L1.d(), Z1.d(), st.as<int>());
+    apply(Z1.d(), A, Q1.d());
+    gram(G.d(), Q1.d());
+    chol_full(h, G.d(), N, 0.0, L2.d(), Z2.d(), st.as<int>() + nb);
+    apply(Z2.d(), Q1.d(), Q);
+    if (wide) gemm(h, RL, N, N, 1.0, L1.d(), N, false, N, L2.d(), N, false);   // L = L1 L2
+    else gemm(h, RL, N, N, 1.0, L2.d(), N, true, N, L1.d(), N, true);         // R = L2^T L1^T
+    if (all_zero(2 * nb)) {
+        res.certified = true;
+        res.cert_ratio = std::sqrt(0.5 * tau_rel);
+        return res;
+    }
+    res.robust = true;
+    const double s_rel = 11.0 * (double(M) * N + double(N) * (N + 1)) * kU;
+    gram(G.d(), A);
+    chol_full(h, G.d(), N, s_rel, L1.d(), Z1.d(), st.as<int>());
+    apply(Z1.d(), A, Q1.d());
+    gram(G.d(), Q1.d());
+    chol_full(h, G.d(), N, 0.0, L2.d(), Z2.d(), st.as<int>() + nb);
+    apply(Z2.d(), Q1.d(), Q2.d());
+    gram(G.d(), Q2.d());
+    chol_full(h, G.d(), N, 0.0, L3.d(), Z3.d(), st.as<int>() + 2 * nb);
+    apply(Z3.d(), Q2.d(), Q);
+    if (wide) {   // L = L1 L2 L3
+        gemm(h, T.d(), N, N, 1.0, L1.d(), N, false, N, L2.d(), N, false);
+        gemm(h, RL, N, N, 1.0, T.d(), N, false, N, L3.d(), N, false);
+    } else {      // R = L3^T L2^T L1^T
+        gemm(h, T.d(), N, N, 1.0, L3.d(), N, true, N, L2.d(), N, true);
+        gemm(h, RL, N, N, 1.0, T.d(), N, false, N, L1.d(), N, true);
+    }
+    if (all_zero(3 * nb)) {
+        gram(T.d(), Q);
+        if (max_abs_dev_identity(h, T.d(), N) <= 64.0 * double(N) * kU) return res;
+    }
+    throw Error{XRS_ENUMERIC, "orthogonalize: a numerically rank-deficient matrix with rank > 512 is not supported"};
+}
+
+// ------------------------------------------------------------------------------------------------
 // CholeskyQR2 / shifted CholeskyQR3. Tall: A (m x n) = Q R. Wide: A (m x n) = L Q.
 OrthResult orthogonalize(xrs_handle_t h, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL) {
     const size_t N = wide ? m : n;   // Gram size
     const size_t M = wide ? n : m;   // long dimension
     XRS_REQUIRE(N >= 1 && M >= N, "orthogonalize: need a tall (or, wide=true, a wide) matrix");
     OrthResult res{false, 0.0, false};
-    if (N > size_t(kSmallMax)) throw Error{XRS_EINVAL, "orthogonalize: rank > 512 not supported yet"};
+    if (N > size_t(kSmallMax)) return orthogonalize_big(h, A, m, n, wide, Q, RL);
     const int Ni = int(N), nvec = int(M);
     DevBuf G(h, N * N * 8), Dv(h, (N + 32) * 32 * 8), L1(h, N * N * 8), Q1(h, m * n * 8), st(h, 64);
     auto gram = [&](double* out, const double* X) {
@@ -260,7 +325,7 @@ static void compact_cols(xrs_handle_t h, double* dst, size_t ldd, const double* 
 size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     const size_t k = std::min(m, n);
-    if (m < n || n > size_t(kSmallMax) || small_problem(m, n)) {
+    if (m < n || small_problem(m, n)) {
         DevBuf Qf(h, m * k * 8);
         const size_t r = qrcp(h, A, m, n, Qf.d(), C, true, false, true);
         compact_cols(h, Q, r, Qf.d(), k, m, r);
@@ -270,6 +335,7 @@ size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double
     // certified: sigma_min >= cert*||A||_F > 16 u R_00 (R_00 <= ||A||_F) -> rank n
     if (o.certified && o.cert_ratio > 64.0 * kDblEps) return n;
     if (!reference_r00_positive(h, A, m, n, false)) return n;  // reference never reduces rank then
+    XRS_REQUIRE(n <= size_t(kSmallMax), "qc: the rank-revealing pivoted QR above 512 columns is not supported");
     // exact pivoted rank on the triangular factor (same column norms as A up to rounding)
     DevBuf Rc(h, n * n * 8), Q2(h, n * n * 8), Cq(h, n * n * 8), Qo(h, m * n * 8);
     XRS_HIP(hipMemcpyAsync(Rc.d(), C, n * n * 8, hipMemcpyDeviceToDevice, h->stream));
@@ -284,7 +350,7 @@ size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double
 size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double* Q) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     const size_t k = std::min(m, n);
-    if (n < m || m > size_t(kSmallMax) || small_problem(m, n)) {
+    if (n < m || small_problem(m, n)) {
         DevBuf At(h, m * n * 8), Qt(h, n * k * 8), Ct(h, k * m * 8);
         transpose(h, At.d(), A, m, n);                           // n x m
         const size_t r = qrcp(h, At.d(), n, m, Qt.d(), Ct.d(), true, false, true);   // A^T = Qt Ct
@@ -297,6 +363,7 @@ size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double
     OrthResult o = orthogonalize(h, A, m, n, true, Q, C);        // A = L Q, C := L (m x m)
     if (o.certified && o.cert_ratio > 64.0 * kDblEps) return m;
     if (!reference_r00_positive(h, A, m, n, true)) return m;
+    XRS_REQUIRE(m <= size_t(kSmallMax), "cq: the rank-revealing pivoted QR above 512 rows is not supported");
     DevBuf Lt(h, m * m * 8), Q2(h, m * m * 8), C2(h, m * m * 8), Qo(h, m * n * 8);
     transpose(h, Lt.d(), C, m, m);                                // A^T = Q^T L^T
     const size_t r = qrcp(h, Lt.d(), m, m, Q2.d(), C2.d(), true, true, true);   // L^T P = Q2 R2
@@ -308,7 +375,7 @@ size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double
 
 void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* R) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
-    if (m >= n && n <= size_t(kSmallMax) && !small_problem(m, n)) {
+    if (m >= n && !small_problem(m, n)) {
         orthogonalize(h, A, m, n, false, Q, R);
         return;
     }
@@ -317,7 +384,7 @@ void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* 
 
 void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* Q) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
-    if (m <= n && m <= size_t(kSmallMax) && !small_problem(m, n)) {
+    if (m <= n && !small_problem(m, n)) {
         orthogonalize(h, A, m, n, true, Q, R);
         return;
     }

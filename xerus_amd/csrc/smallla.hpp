@@ -89,6 +89,10 @@ void solve_dense(xrs_handle_t h, double* X, const double* A, size_t m, size_t n,
 void svd_solve(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
 bool chol_blocked(xrs_handle_t h, const double* A, size_t n, double* L, std::vector<DevBuf>& Z);
 void chol_solve(xrs_handle_t h, const double* L, const std::vector<DevBuf>& Z, size_t n, const double* B, size_t p, double* X);
+// Cholesky of A + shift_rel tr(A) I for any n, enqueued only: status[0 .. chol_full_blocks(n)) (all zero on
+// success), optional L (lower) and Z = L^{-1} (n x n each)
+int chol_full_blocks(size_t n);
+void chol_full(xrs_handle_t h, const double* A, size_t n, double shift_rel, double* L, double* Z, int* status);
 
 // helpers
 void transpose(xrs_handle_t h, double* out, const double* in, size_t rows, size_t cols);

@@ -112,6 +112,68 @@ bool chol_blocked(xrs_handle_t h, const double* A, size_t n, double* L, std::vec
     return true;
 }
 
+namespace {
+// W[i][i] += rel * trace(W) (one workgroup; the shifted factorisations of the certificates)
+__global__ void __launch_bounds__(256) k_shift_diag(double* __restrict__ W, size_t n, double rel) {
+    __shared__ double red[4];
+    double tr = 0.0;
+    for (size_t i = threadIdx.x; i < n; i += 256) tr += W[i * n + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tr += __shfl_xor(tr, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = tr;
+    __syncthreads();
+    const double s = rel * ((red[0] + red[1]) + (red[2] + red[3]));
+    for (size_t i = threadIdx.x; i < n; i += 256) W[i * n + i] += s;
+}
+}  // namespace
+
+int chol_full_blocks(size_t n) { return int((n + kCholBlock - 1) / kCholBlock); }
+
+// Cholesky of A + shift_rel tr(A) I of any order, enqueued only: status[b] = potrf status of diagonal
+// block b (chol_full_blocks(n) slots, all zero on success); L (n x n lower, upper zero) and the full
+// inverse Z = L^{-1} (block forward substitution: Z_ii = L_ii^{-1}, Z_ij = -Z_ii L_i,<i Z_<i,j) when
+// the pointers are given. The TT drivers use it for ranks above the batched kernels' 512.
+void chol_full(xrs_handle_t h, const double* A, size_t n, double shift_rel, double* L, double* Z, int* status) {
+    const size_t nblk = size_t(chol_full_blocks(n));
+    DevBuf W(h, n * n * 8), Lown(h, L ? 8 : n * n * 8), D(h, size_t(kCholBlock) * kCholBlock * 8),
+        Dinv(h, dinv_elems(kCholBlock) * 8), P(h, n * kCholBlock * 8), T(h, n * n * 8);
+    double* Lm = L ? L : Lown.d();
+    XRS_HIP(hipMemcpyAsync(W.d(), A, n * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    if (shift_rel != 0.0) {
+        hipLaunchKernelGGL(k_shift_diag, dim3(1), dim3(256), 0, h->stream, W.d(), n, shift_rel);
+        check_launch("k_shift_diag");
+    }
+    XRS_HIP(hipMemsetAsync(Lm, 0, n * n * 8, h->stream));
+    if (Z) XRS_HIP(hipMemsetAsync(Z, 0, n * n * 8, h->stream));
+    DevBuf Zb(h, size_t(kCholBlock) * kCholBlock * 8);
+    for (size_t jb = 0; jb < nblk; ++jb) {
+        const size_t j0 = jb * kCholBlock, b = std::min<size_t>(kCholBlock, n - j0), rest = n - j0 - b;
+        copy2d(h, D.d(), b, W.d() + j0 * n + j0, n, b, b);
+        potrf(h, D.d(), int(b), 0.0, Dinv.d(), status + jb);
+        TrinvBatch tb{};
+        tb.L[0] = D.d();
+        tb.Dinv[0] = Dinv.d();
+        tb.X[0] = Zb.d();
+        tb.n[0] = int(b);
+        trinv_batched(h, tb, 1);
+        copy2d(h, Lm + j0 * n + j0, n, D.d(), b, b, b);
+        if (Z) {
+            copy2d(h, Z + j0 * n + j0, n, Zb.d(), b, b, b);
+            if (j0) {   // Z[j, :j0] = -Z_jj (L[j, :j0] Z[:j0, :j0])
+                gemm(h, T.d(), b, j0, 1.0, Lm + j0 * n, n, false, j0, Z, n, false);
+                gemm(h, P.d(), b, j0, -1.0, Zb.d(), b, false, b, T.d(), j0, false);
+                copy2d(h, Z + j0 * n, n, P.d(), j0, b, j0);
+            }
+        }
+        if (!rest) break;
+        gemm(h, P.d(), rest, b, 1.0, W.d() + (j0 + b) * n + j0, n, false, b, Zb.d(), b, true);   // L_ij = W_ij Z_jj^T
+        copy2d(h, Lm + (j0 + b) * n + j0, n, P.d(), b, rest, b);
+        gemm_sym(h, T.d(), rest, 1.0, P.d(), b, false, b, P.d(), b, true);
+        const size_t od[2] = {n, n}, id[2] = {rest, rest}, off[2] = {j0 + b, j0 + b};
+        offset_add(h, W.d(), od, T.d(), id, 2, off, -1.0);
+    }
+}
+
 // X (n x p) = (L L^T)^{-1} B with the factors of chol_blocked
 void chol_solve(xrs_handle_t h, const double* L, const std::vector<DevBuf>& Z, size_t n, const double* B, size_t p, double* X) {
     const size_t nblk = Z.size();

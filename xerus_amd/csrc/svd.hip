@@ -581,7 +581,8 @@ void launch_blocks(xrs_handle_t h, const double* W, int ldw, bool trans, int p, 
 
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
                int* status_dev, int max_sweeps, int kernel) {
-    XRS_REQUIRE(p >= 1 && p <= SV_MAXP && p <= q, "jacobi_vt: need 1 <= p <= min(q, 512)");
+    XRS_REQUIRE(p >= 1 && p <= q && (p <= SV_MAXP || (q <= 2 * SVB_QMAX && kernel != 1)),
+                "jacobi_vt: need 1 <= p <= q, p <= 512 (one workgroup) or q <= 1024 (blocks)");
     XRS_REQUIRE(kernel >= 0 && kernel <= 2, "jacobi_vt: kernel is 0 (auto), 1 (one workgroup) or 2 (blocks)");
     KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * q * 6.0, 16.0 * double(p) * q);
     // smallest p handed to the multi-workgroup block kernel (XRS_SVD_BLOCK_MIN tunes it; measured faster
@@ -590,9 +591,11 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
         const char* e = std::getenv("XRS_SVD_BLOCK_MIN");
         return e ? std::atoi(e) : 32;
     }();
-    const bool blocks_ok = q <= SVB_QMAX;
-    XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 512");
-    if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
+    const bool blocks_ok = q <= 2 * SVB_QMAX;
+    XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 1024");
+    if (q > SVB_QMAX) {   // rows of up to 1024 columns: blocks of 8 rows (2 x 8 x 1024 doubles of LDS)
+        launch_blocks<8, 32, 32, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+    } else if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
         // register tiling E * 32 columns: the narrowest that holds q (padding costs FMAs and LDS traffic)
         if (q <= 64) launch_blocks<16, 32, 2, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
         else if (q <= 128) launch_blocks<16, 32, 4, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);

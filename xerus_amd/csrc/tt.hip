@@ -572,12 +572,20 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     std::vector<double*> dinv(d, nullptr);
     struct Job { const double* src; double* G; double* Dinv; double shift; int n; };
     std::vector<Job> jobs;
-    std::vector<BigJob> big;
+    std::vector<BigJob> big, huge;   // huge: r > 512, blocked Cholesky one job at a time
     DevBuf Dv(h, dsz * 8 + 8), Dscr(h, (certify ? 2 * dsz : 1) * 8 + 8);
     size_t off = 0;
     for (size_t k = 1; k < d; ++k) {
         const size_t a = t.r[k];
         Lf[k] = DevBuf(h, a * a * 8);
+        if (a > 512) {
+            huge.push_back({H[k], 0.0, int(a), Lf[k].d(), Z[k].d()});
+            if (certify) {
+                huge.push_back({G[k], -kGramShift, int(a), nullptr, nullptr});
+                huge.push_back({H[k], -kGramShift, int(a), nullptr, nullptr});
+            }
+            continue;
+        }
         if (a > 256) {
             big.push_back({H[k], 0.0, int(a), Lf[k].d(), Z[k].d()});
             if (certify) {
@@ -596,8 +604,17 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
         off += de;
     }
     const int cnt_small = int(jobs.size());
-    const int cnt = cnt_small + 2 * int(big.size());
+    int cnt_huge = 0;
+    for (const BigJob& j : huge) cnt_huge += chol_full_blocks(size_t(j.n));
+    const int cnt = cnt_small + 2 * int(big.size()) + cnt_huge;
     DevBuf st(h, size_t(cnt) * 4 + 64);
+    {
+        int slot = cnt_small + 2 * int(big.size());
+        for (const BigJob& j : huge) {
+            chol_full(h, j.src, size_t(j.n), j.shift_rel, j.L, j.Z, st.as<int>() + slot);
+            slot += chol_full_blocks(size_t(j.n));
+        }
+    }
     for (size_t b0 = 0; b0 < big.size(); b0 += kBigMax) {   // chunks of the kernels' argument tables
         const std::vector<BigJob> part(big.begin() + long(b0), big.begin() + long(std::min(big.size(), b0 + kBigMax)));
         factor_big(h, part, st.as<int>() + cnt_small + 2 * b0, Cs);
@@ -729,7 +746,7 @@ bool round_chain(TT& t, const size_t* max_ranks, double eps) {
     static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
     if (d < 2 || d > 65 || (!t.sharded() && exceeds_maximal_ranks(t))) return false;
     for (size_t k = 1; k < d; ++k)
-        if (t.r[k] > max_ranks[k - 1] || t.r[k] > size_t(kSmallMax)) return false;
+        if (t.r[k] > max_ranks[k - 1] || t.r[k] > kHugeMax) return false;
     const double cX = 0.5 * std::sqrt(kGramShift);
     if (!(eps < 0.25 * cX * cX)) return false;
     // factorisation statuses (<= 3*64 ints) in a region of the pinned scratch no other routine uses

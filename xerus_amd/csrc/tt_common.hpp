@@ -74,6 +74,9 @@ void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs);
 
 // Cholesky (+ explicit inverse) of 256 < n <= 512 matrices from the n <= 256 kernels (2 x 2 blocks)
 constexpr int kBigMax = 64;
+// largest rank of the certified chain / truncating rounds (blocked Cholesky above 512, the 1024-column
+// register tiling of the block Jacobi SVD)
+constexpr size_t kHugeMax = 1024;
 struct BigJob {
     const double* src;
     double shift_rel;

@@ -64,7 +64,8 @@ struct Sweep {
     }
 };
 
-// one or more Cholesky factorisations of an n x n symmetric matrix in a single launch (n <= 512):
+// one or more Cholesky factorisations of an n x n symmetric matrix in a single launch (n <= 512; larger
+// ones blocked, one job at a time):
 // the factor L (lower, out of place) and its inverse Z = L^{-1}, plus status-only certificates
 // chol(A - tau tr(A) I). Statuses go to status[0..count).
 struct CholJob {
@@ -81,8 +82,13 @@ void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
     PotrfBatch pb{};
     TrinvBatch tb{};
     int ns = 0, ninv = 0;
+    std::vector<int> huge;
     for (size_t i = 0; i < jobs.size(); ++i) {
         const CholJob& j = jobs[i];
+        if (j.n > 512) {   // blocked, one job at a time (ranks above the batched kernels)
+            huge.push_back(int(i));
+            continue;
+        }
         if (j.n > 256) {
             big.push_back({j.A, j.L ? 0.0 : -kGramShift, j.n, j.L, j.Z});
             big_slot.push_back(int(i));
@@ -116,11 +122,17 @@ void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
         factor_big(h, big, status + ns, keep);
         for (auto& k : keep) sw.keep.push_back(std::move(k));
     }
+    int slot = ns + 2 * int(big.size());
+    for (int i : huge) {
+        const CholJob& j = jobs[size_t(i)];
+        chol_full(h, j.A, size_t(j.n), j.L ? 0.0 : -kGramShift, j.L, j.Z, status + slot);
+        slot += chol_full_blocks(size_t(j.n));
+    }
 }
 
 int chol_status_count(const std::vector<CholJob>& jobs) {
     int c = 0;
-    for (const CholJob& j : jobs) c += j.n > 256 ? 2 : 1;
+    for (const CholJob& j : jobs) c += j.n > 512 ? chol_full_blocks(size_t(j.n)) : (j.n > 256 ? 2 : 1);
     return c;
 }
 
@@ -220,7 +232,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     const double cX = 0.5 * std::sqrt(kGramShift);
     if (!(eps < 0.25 * cX * cX)) return false;
     for (size_t k = 1; k < d; ++k)
-        if (t.r[k] > size_t(kSmallMax)) return false;
+        if (t.r[k] > kHugeMax) return false;
 
     // 1a. structural excess (a wide left unfolding, r_{k+1} > r_k n_k, e.g. the boundary edges of x + y):
     //     the reference's own QC steps there (exact rank rule, host syncs)
