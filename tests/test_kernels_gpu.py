@@ -71,6 +71,11 @@ GEMMS = [
     (5120, 256, 256, False, False),  # R * core
     (256, 256, 5120, False, True),   # Gram of a wide core
     (128, 2560, 128, True, True),
+    # whole-tile shapes of the LDS-DMA pipeline (k_gemm_glds): 64x80 / 80x64 / 64x64 / 32x32 tiles, every
+    # transpose combination
+    (256, 5120, 256, False, False), (256, 5120, 256, False, True), (5120, 256, 256, True, True),
+    (5120, 256, 256, True, False), (512, 10240, 512, False, False), (320, 640, 96, True, False),
+    (64, 160, 64, False, True), (96, 96, 64, True, True),
     (1, 37, 19, False, False), (37, 1, 19, True, False), (13, 17, 1, False, True),
     (100, 3, 7, True, True), (129, 131, 67, False, False), (65, 63, 2000, True, True),
 ]

@@ -24,7 +24,10 @@ TORCH = len(sys.argv) > 1 and sys.argv[1] == "torch"   # separate process: one H
 h = None if TORCH else capi.Handle(0)
 rng = np.random.default_rng(0)
 cfg = os.environ.get("XRS_GEMM_CFG", "default")
+ONLY = os.environ.get("XRS_BENCH_ONLY")   # substring filter on the shape description
 for M, N, K, ta, tb, what in ([] if TORCH else SHAPES):
+    if ONLY and ONLY not in what:
+        continue
     A = h.array(rng.standard_normal((K, M) if ta else (M, K)))
     B = h.array(rng.standard_normal((N, K) if tb else (K, N)))
     C = h.empty((M, N))

@@ -13,7 +13,7 @@ from typing import Sequence
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libxerus_amd.so")
+LIB_PATH = os.environ.get("XRS_LIB_PATH") or os.path.join(_HERE, "libxerus_amd.so")   # (override: diagnostic builds)
 
 _SZ = C.c_size_t
 _DP = C.c_void_p

@@ -29,16 +29,16 @@ struct GemmOne {
     const double* A;
     const double* B;
     double* C;
-    __device__ const double* a(int) const { return A; }
-    __device__ const double* b(int) const { return B; }
+    __host__ __device__ const double* a(int) const { return A; }
+    __host__ __device__ const double* b(int) const { return B; }
     __device__ double* c(int) const { return C; }
 };
 struct GemmMany {
     const double* A[kGemmBatchMax];
     const double* B[kGemmBatchMax];
     double* C[kGemmBatchMax];
-    __device__ const double* a(int i) const { return A[i]; }
-    __device__ const double* b(int i) const { return B[i]; }
+    __host__ __device__ const double* a(int i) const { return A[i]; }
+    __host__ __device__ const double* b(int i) const { return B[i]; }
     __device__ double* c(int i) const { return C[i]; }
 };
 
@@ -47,16 +47,173 @@ struct GemmMany {
 template <int BM, int BN, int WGM, int WGN, int WGK>
 constexpr int gemm_min_waves() { return (BM * BN >= 128 * 128) ? 2 : 4; }
 
+#ifdef XRS_GEMM_TRACE
+// Diagnostic build only (tools/gemm_trace.py): per workgroup {start, end, XCC_ID << 32 | HW_ID} in
+// s_memrealtime ticks (100 MHz), written by thread 0 of each workgroup.
+__device__ unsigned long long* g_gemm_trace = nullptr;
+__device__ unsigned long long* g_gemm_steps = nullptr;   // glds kernel: s_memtime after each K-step barrier
+#define XRS_TRACE_BEGIN                                                   \
+    const unsigned long long xrs_t0 = __builtin_amdgcn_s_memrealtime();  \
+    const unsigned long long xrs_c0 = __builtin_amdgcn_s_memtime();
+#define XRS_TRACE_STEP(t)                                                                                   \
+    if (threadIdx.x == 0 && g_gemm_steps != nullptr && (t) < 15) {                                          \
+        const size_t wg = blockIdx.x + size_t(gridDim.x) * (blockIdx.y + size_t(gridDim.y) * blockIdx.z);   \
+        g_gemm_steps[16 * wg + (t)] = __builtin_amdgcn_s_memtime() - xrs_c0;                                \
+    }
+#define XRS_TRACE_END                                                                                     \
+    if (threadIdx.x == 0 && g_gemm_trace != nullptr) {                                                    \
+        const size_t wg = blockIdx.x + size_t(gridDim.x) * (blockIdx.y + size_t(gridDim.y) * blockIdx.z); \
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();                                   \
+        const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    /* HW_REG_HW_ID */             \
+        const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  /* HW_REG_XCC_ID */            \
+        g_gemm_trace[3 * wg] = xrs_t0;                                                                   \
+        g_gemm_trace[3 * wg + 1] = t1;                                                                   \
+        g_gemm_trace[3 * wg + 2] = (static_cast<unsigned long long>(xcc) << 32) | hw;                    \
+        if (g_gemm_steps != nullptr) g_gemm_steps[16 * wg + 15] = __builtin_amdgcn_s_memtime() - xrs_c0;  \
+    }
+#else
+#define XRS_TRACE_BEGIN
+#define XRS_TRACE_END
+#define XRS_TRACE_STEP(t)
+#endif
+
+template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB, class PTR>
+__device__ __forceinline__ void gemm_body(const PTR& ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
+                                          double alpha, double* __restrict__ slab, int tiles_m, int xcd_group,
+                                          int* __restrict__ tickets, int sym);
+
 template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB, class PTR>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64, (gemm_min_waves<BM, BN, WGM, WGN, WGK>()))
 k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
            double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym) {
+    XRS_TRACE_BEGIN
+    gemm_body<BM, BN, GBK, WGM, WGN, WGK, PD, TA, TB, PTR>(ptrs, lda, ldb, M, N, K, kps, alpha, slab, tiles_m,
+                                                          xcd_group, tickets, sym);
+    XRS_TRACE_END
+}
+
+// Accumulators -> C: sums the NACC accumulator sets, reduces the WGK wave groups through LDS (`lds`, at
+// least (WGK-1) * WGM * WGN * TM * TN * 256 doubles, free to overwrite), then stores C (alpha, symmetric
+// mirror), a split-K slab, or a slab + the in-launch combine (tickets). Shared by both GEMM kernels.
+template <int TM, int TN, int WGM, int WGN, int WGK, int NACC, class PTR>
+__device__ __forceinline__ void gemm_finish(d4 (&acc2)[NACC][TM][TN], double* lds, const PTR& ptrs, int M, int N,
+                                            double alpha, double* __restrict__ slab, int* __restrict__ tickets,
+                                            int sym, int m0, int n0, int wm, int wn, int kg, int pos) {
+    const int bz = blockIdx.y;
+    double* __restrict__ C = ptrs.c(bz);
+    const int zslice = bz * int(gridDim.z) + int(blockIdx.z);
+    const int tslot = bz * int(gridDim.x) + int(blockIdx.x);
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const bool mirror = sym != 0;
+    d4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            acc[i][j] = acc2[0][i][j];
+            if constexpr (NACC > 1) acc[i][j] += acc2[1][i][j];
+        }
+    // ---- intra-workgroup K reduction (wave groups 1.. -> LDS -> group 0)
+    if constexpr (WGK > 1) {
+        double* red = lds;
+        if (kg > 0) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        red[((((kg - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane] = acc[i][j][r];
+        }
+        __syncthreads();
+        if (kg > 0 && tickets == nullptr) return;   // (with tickets every wave stays for the barriers below)
+        if (kg == 0)
+#pragma unroll
+        for (int g = 1; g < WGK; ++g)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        acc[i][j][r] += red[((((g - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane];
+    }
+    // ---- epilogue
+    const bool to_slab = slab != nullptr;
+    const size_t MN = size_t(M) * size_t(N);
+    double* out = to_slab ? slab + size_t(zslice) * MN : C;
+    const double scale = to_slab ? 1.0 : alpha;
+    const int lc = lane & 15, lg = lane >> 4;
+    if (kg == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = n0 + wn + j * 16 + lc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wm + i * 16 + lg + 4 * r;
+                    if (row < M && col < N) {
+                        if (tickets != nullptr)   // write-through (sc1): visible to any XCD without a release fence
+                            __hip_atomic_store(&out[size_t(row) * N + col], acc[i][j][r], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        else if (!mirror || to_slab)
+                            out[size_t(row) * N + col] = scale * acc[i][j][r];
+                        else if (row >= col) {
+                            out[size_t(row) * N + col] = scale * acc[i][j][r];
+                            out[size_t(col) * N + row] = scale * acc[i][j][r];
+                        }
+                    }
+                }
+            }
+    }
+    if (tickets == nullptr) return;
+    // ---- in-launch split-K combine (cdna_hip_programming.md §5 projection-GEMM item 2, sc1 form): every
+    // slice stores its slab write-through (sc1, above), drains its stores and draws a ticket; the slice
+    // that draws splits-1 reads the other slabs with sc1 loads (no fences anywhere) and sums them in
+    // slice order 0..splits-1 -- the order of k_splitk_reduce, so both forms are bitwise identical.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    double* flag = lds;   // the one LDS array (no second __shared__ object, see the guide's trap 4a)
+    if (tid == 0) {
+        const int t = __hip_atomic_fetch_add(&tickets[tslot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool last = (t == int(gridDim.z) - 1);
+        if (last) __hip_atomic_store(&tickets[tslot], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag[0] = last ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (flag[0] == 0.0 || kg != 0) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn + j * 16 + lc;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = m0 + wm + i * 16 + lg + 4 * r;
+                if (row < M && col < N && (!mirror || row >= col)) {
+                    const size_t o = size_t(row) * N + col;
+                    double sum = 0.0;
+                    for (int z = 0; z < int(gridDim.z); ++z)
+                        sum += (z == int(blockIdx.z)) ? acc[i][j][r]
+                                                      : __hip_atomic_load(&slab[(size_t(bz) * gridDim.z + z) * MN + o], __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT);
+                    C[o] = alpha * sum;
+                    if (mirror) C[size_t(col) * N + row] = alpha * sum;
+                }
+            }
+        }
+}
+
+
+template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, bool TA, bool TB, class PTR>
+__device__ __forceinline__ void gemm_body(const PTR& ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
+                                          double alpha, double* __restrict__ slab, int tiles_m, int xcd_group,
+                                          int* __restrict__ tickets, int sym) {
     const int bz = blockIdx.y;   // batch entry
     const double* __restrict__ A = ptrs.a(bz);
     const double* __restrict__ B = ptrs.b(bz);
-    double* __restrict__ C = ptrs.c(bz);
-    const int zslice = bz * int(gridDim.z) + int(blockIdx.z);   // this slice's slab index
-    const int tslot = bz * int(gridDim.x) + int(blockIdx.x);    // this tile's ticket
     constexpr int NT = WGM * WGN * WGK * 64;   // WGK wave groups split every K-step's MFMA k-substeps
     // LDS rows of BM / BN doubles, XOR-swizzled per k row: element (k, m) at k*SA + (m ^ swz(k)) with
     // swz(k) = 16*(k&1) | (k&15). ds_read_b64 banks over 32-lane groups, (a/4) mod 64: the fragment reads
@@ -113,7 +270,6 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
     // symmetric result (sym, square tiles, M == N): only tiles on or below the diagonal are computed;
     // each lower element is also written to its mirror position
     if (sym && tm < tn) return;
-    const bool mirror = sym != 0;
     const int m0 = tm * BM, n0 = tn * BN;
     const int kbeg = blockIdx.z * kps;
     const int kend = min(K, kbeg + kps);
@@ -241,104 +397,209 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
         }
     }
 
-    d4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            acc[i][j] = acc2[0][i][j];
-            if constexpr (NACC > 1) acc[i][j] += acc2[1][i][j];
-        }
-    // ---- intra-workgroup K reduction (wave groups 1.. -> LDS -> group 0)
-    if constexpr (WGK > 1) {
-        double* red = &As[0][0];
-        if (kg > 0) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        red[((((kg - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane] = acc[i][j][r];
-        }
-        __syncthreads();
-        if (kg > 0 && tickets == nullptr) return;   // (with tickets every wave stays for the barriers below)
-        if (kg == 0)
-#pragma unroll
-        for (int g = 1; g < WGK; ++g)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        acc[i][j][r] += red[((((g - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane];
+    gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, &As[0][0], ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// k_gemm_glds: the pipeline for whole tiles (M % BM == N % BN == 0, K-slices of whole 32-deep steps,
+// 16-B aligned operands). Operands go global -> LDS by 16-B global_load_lds (LDS-DMA, no VGPR staging)
+// into S = 3 LDS stages; one raw s_barrier per 32-deep K-step, preceded by a counted vmcnt that leaves the
+// next stage's DMA in flight across it (cdna_hip_programming.md §5 "Pipelining across barriers"). The
+// DMA destination is lane-linear, so the bank swizzle goes on the SOURCE address:
+//   RK image (operand stored [r][k], k contiguous): row r = 32 doubles, 16-B chunk c at c ^ (r & 15)
+//   KR image (operand stored [k][r], R doubles per k row): chunk c of row k at c ^ (8 (k & 1)) (R % 32 == 0)
+// Fragment reads (16 rows x k, k+1 per 32-lane half) then hit 32 distinct 8-B bank pairs in both images.
+constexpr int kGldsBK = 32;
+
+template <int R, bool KMAJ>
+struct GldsImg {
+    // k-major rows of R % 32 == 16 doubles alternate bank halves by themselves (640-B rows: k*160 words mod 64 =
+    // 0, 32, ...); rows of whole 256-B bank rows take the XOR
+    static_assert(!KMAJ || R % 16 == 0, "k-major image rows must be whole MFMA tiles");
+    static constexpr int KSWZ = (R % 32 == 0) ? 8 : 0;
+    static constexpr int DOUBLES = R * kGldsBK;
+    static constexpr int INSTR = DOUBLES * 8 / 1024;   // 1-KB wave instructions per stage
+    __device__ static int at(int r, int k) {   // LDS offset (doubles) of element (r, k)
+        if constexpr (!KMAJ) return r * kGldsBK + ((((k >> 1) ^ (r & 15))) << 1) + (k & 1);
+        else return k * R + ((((r >> 1) ^ ((k & 1) * KSWZ))) << 1) + (r & 1);
     }
-    // ---- epilogue
-    const bool to_slab = slab != nullptr;
-    const size_t MN = size_t(M) * size_t(N);
-    double* out = to_slab ? slab + size_t(zslice) * MN : C;
-    const double scale = to_slab ? 1.0 : alpha;
-    const int lc = lane & 15, lg = lane >> 4;
-    if (kg == 0) {
+    // Per-lane fragment offsets of the NF 16-row MFMA fragments at rows w0 + 16 i (w0 % 16 == 0) for
+    // K-substep q of a wave group kg (of WGK, a power of 2): lane (lr = l & 15, lk = l >> 4) reads element
+    // (w0 + 16 i + lr, kk = 4 (q WGK + kg) + lk). The q dependence reduces to a compile-time term (an
+    // immediate ds_read offset for KR images; one XOR for RK images, whose 16-B chunk index 2 (q WGK + kg)
+    // + (lk >> 1) equals (2 q WGK) ^ (2 kg) ^ (lk >> 1) because the bit ranges are disjoint).
+    template <int NF, int WGK>
+    struct Frag {
+        static_assert((WGK & (WGK - 1)) == 0, "wave groups must be a power of 2");
+        int base[KMAJ ? NF : 1];
+        int z = 0;
+        __device__ Frag(int w0, int kg, int lane) {
+            const int lr = lane & 15, lk = lane >> 4;
+            if constexpr (!KMAJ) {
+                base[0] = (w0 + lr) * kGldsBK + (lk & 1);
+                z = (2 * kg) ^ (lk >> 1) ^ lr;
+            } else {
+                const int swz = (lk & 1) * (KSWZ / 8);
+#pragma unroll
+                for (int i = 0; i < NF; ++i) base[i] = (4 * kg + lk) * R + 16 * ((w0 / 16 + i) ^ swz) + lr;
+            }
+        }
+        __device__ int off(int q, int i) const {
+            if constexpr (!KMAJ) return base[0] + i * 16 * kGldsBK + (((2 * q * WGK) ^ z) << 1);
+            else return base[i] + 4 * q * WGK * R;
+        }
+    };
+    __device__ static void src(int q, int& r, int& k) {   // element (r, k) that starts LDS chunk q
+        if constexpr (!KMAJ) {
+            r = q >> 4;
+            k = ((q & 15) ^ (r & 15)) << 1;
+        } else {
+            constexpr int CR = R / 2;
+            k = q / CR;
+            r = ((q % CR) ^ ((k & 1) * KSWZ)) << 1;
+        }
+    }
+};
+
+template <int BM, int BN, int WGM, int WGN, int WGK>
+constexpr int glds_min_waves() { return (WGM * WGN * WGK * 64 >= 512) ? 2 : 1; }
+
+template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR>
+__global__ void __launch_bounds__(WGM * WGN * WGK * 64, (glds_min_waves<BM, BN, WGM, WGN, WGK>()))
+k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
+            double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym) {
+    XRS_TRACE_BEGIN
+    constexpr int BK = kGldsBK, S = 3;
+    constexpr int NW = WGM * WGN * WGK;
+    using IA = GldsImg<BM, TA>;   // A stored [m][k] (RK) or, transposed, [k][m] (KR)
+    using IB = GldsImg<BN, !TB>;  // B stored [k][n] (KR) or, transposed, [n][k] (RK)
+    constexpr int STAGE = IA::DOUBLES + IB::DOUBLES;
+    constexpr int INSTR = IA::INSTR + IB::INSTR;
+    // wave w issues DMA instructions j = w, w + NW, ...: PER_WAVE of them, or one fewer for w >= INSTR % NW
+    constexpr int PER_WAVE = (INSTR + NW - 1) / NW;
+    static_assert(PER_WAVE * (S - 2) <= 63, "vmcnt range");
+    constexpr int WM = BM / WGM, WN = BN / WGN;
+    constexpr int TM = WM / 16, TN = WN / 16;
+    static_assert(TM >= 1 && TN >= 1 && WM % 16 == 0 && WN % 16 == 0, "wave tile must be whole MFMA tiles");
+    static_assert(BK % (4 * WGK) == 0, "K-step must split evenly over the wave groups");
+    constexpr int NACC = (TM * TN <= 2) ? 2 : 1;
+    static_assert(WGK == 1 || (WGK - 1) * WGM * WGN * TM * TN * 256 <= S * STAGE, "LDS reduction buffer too small");
+    __shared__ double lds[S * STAGE];   // the one LDS array (trap 4a: no second __shared__ object)
+
+    const int bz = blockIdx.y;
+    const double* __restrict__ A = ptrs.a(bz);
+    const double* __restrict__ B = ptrs.b(bz);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int kg = wave / (WGM * WGN), pos = wave % (WGM * WGN);
+    const int wm = (pos / WGN) * WM, wn = (pos % WGN) * WN;
+    int tm, tn;
+    if (sym) {   // the grid holds the lower tiles only: x -> (tm, tn), tm >= tn, row by row
+        const int x = blockIdx.x;
+        tm = int((__builtin_sqrtf(8.0f * float(x) + 1.0f) - 1.0f) * 0.5f);
+        while ((tm + 1) * (tm + 2) / 2 <= x) ++tm;
+        while (tm * (tm + 1) / 2 > x) --tm;
+        tn = x - tm * (tm + 1) / 2;
+    } else {
+        const int b = blockIdx.x, tiles_n = gridDim.x / tiles_m;
+        if (xcd_group == 1) {
+            const int xcd = b & 7, slot = b >> 3;
+            tn = (slot / tiles_m) * 8 + xcd;
+            tm = slot % tiles_m;
+        } else if (xcd_group == 2) {
+            const int xcd = b & 7, slot = b >> 3;
+            tm = (slot / tiles_n) * 8 + xcd;
+            tn = slot % tiles_n;
+        } else {
+            tm = b % tiles_m;
+            tn = b / tiles_m;
+        }
+    }
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = blockIdx.z * kps;
+    const int nsteps = max(0, min(K, kbeg + kps) - kbeg) / BK;   // (the host guarantees whole steps)
+    const bool full = wave < INSTR % NW || INSTR % NW == 0;     // issues PER_WAVE DMAs per stage (else one fewer)
+
+    // this wave's DMA instructions: j = wave + NW u; j < IA::INSTR -> A image, else B image
+    const double* gsrc[PER_WAVE];
+    size_t gstep[PER_WAVE];   // source advance per K-step (doubles)
+    int ldsoff[PER_WAVE];     // LDS destination (doubles) of the instruction within a stage
+#pragma unroll
+    for (int u = 0; u < PER_WAVE; ++u) {
+        const int j = min(wave + NW * u, INSTR - 1);   // (a wave with one fewer never issues its last slot)
+        int r, k;
+        if (j < IA::INSTR) {
+            IA::src((j * 64) + lane, r, k);
+            gsrc[u] = TA ? A + size_t(kbeg + k) * lda + (m0 + r) : A + size_t(m0 + r) * lda + (kbeg + k);
+            gstep[u] = TA ? size_t(BK) * lda : size_t(BK);
+            ldsoff[u] = j * 128;
+        } else {
+            IB::src(((j - IA::INSTR) * 64) + lane, r, k);
+            gsrc[u] = TB ? B + size_t(n0 + r) * ldb + (kbeg + k) : B + size_t(kbeg + k) * ldb + (n0 + r);
+            gstep[u] = TB ? size_t(BK) : size_t(BK) * ldb;
+            ldsoff[u] = IA::DOUBLES + (j - IA::INSTR) * 128;
+        }
+    }
+    auto issue = [&](int t) {   // DMA of K-step t into stage t % S
+        double* st = lds + (t % S) * STAGE;
+#pragma unroll
+        for (int u = 0; u < PER_WAVE; ++u)
+            if (u < PER_WAVE - 1 || full)
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(gsrc[u] + size_t(t) * gstep[u]),
+                                             (__attribute__((address_space(3))) void*)(st + ldsoff[u]),
+                                             16, 0, 0);
+    };
+
+    d4 acc2[NACC][TM][TN];
+#pragma unroll
+    for (int a = 0; a < NACC; ++a)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int col = n0 + wn + j * 16 + lc;
+            for (int j = 0; j < TN; ++j) acc2[a][i][j] = d4{0.0, 0.0, 0.0, 0.0};
+    const typename IA::template Frag<TM, WGK> fa(wm, kg, lane);
+    const typename IB::template Frag<TN, WGK> fb(wn, kg, lane);
+
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m0 + wm + i * 16 + lg + 4 * r;
-                    if (row < M && col < N) {
-                        if (tickets != nullptr)   // write-through (sc1): visible to any XCD without a release fence
-                            __hip_atomic_store(&out[size_t(row) * N + col], acc[i][j][r], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                        else if (!mirror || to_slab)
-                            out[size_t(row) * N + col] = scale * acc[i][j][r];
-                        else if (row >= col) {
-                            out[size_t(row) * N + col] = scale * acc[i][j][r];
-                            out[size_t(col) * N + row] = scale * acc[i][j][r];
-                        }
-                    }
-                }
-            }
-    }
-    if (tickets == nullptr) return;
-    // ---- in-launch split-K combine (cdna_hip_programming.md §5 projection-GEMM item 2, sc1 form): every
-    // slice stores its slab write-through (sc1, above), drains its stores and draws a ticket; the slice
-    // that draws splits-1 reads the other slabs with sc1 loads (no fences anywhere) and sums them in
-    // slice order 0..splits-1 -- the order of k_splitk_reduce, so both forms are bitwise identical.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    double* flag = &As[0][0];   // the one LDS array (no second __shared__ object, see the guide's trap 4a)
-    if (tid == 0) {
-        const int t = __hip_atomic_fetch_add(&tickets[tslot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const bool last = (t == int(gridDim.z) - 1);
-        if (last) __hip_atomic_store(&tickets[tslot], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        flag[0] = last ? 1.0 : 0.0;
-    }
-    __syncthreads();
-    if (flag[0] == 0.0 || kg != 0) return;
+    for (int s = 0; s < S - 1; ++s)
+        if (s < nsteps) issue(s);
+    for (int t = 0; t < nsteps; ++t) {
+        // retire stage t (this wave's DMAs); the next stage's stay in flight across the barrier
+        if (t + 1 >= nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE * (S - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PER_WAVE - 1) * (S - 2)) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of stage t-1 are done
+        __builtin_amdgcn_s_barrier();
+        XRS_TRACE_STEP(t)
+        const double* as = lds + (t % S) * STAGE;
+        const double* bs = as + IA::DOUBLES;
+        // fragments double-buffered in registers: the reads of substep q+1 are issued ahead of the MFMAs of
+        // substep q, so the LDS latency hides behind the MFMA pipe instead of draining it every substep
+        constexpr int NQ = BK / (4 * WGK);
+        double af[2][TM], bf[2][TN];
+        auto frag = [&](int q, double(&a)[TM], double(&b)[TN]) {
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+            for (int i = 0; i < TM; ++i) a[i] = as[fa.off(q, i)];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn + j * 16 + lc;
+            for (int j = 0; j < TN; ++j) b[j] = bs[fb.off(q, j)];
+        };
+        frag(0, af[0], bf[0]);
+#ifndef XRS_GLDS_NOLOAD   // (diagnostic builds: compute-only timing, results meaningless)
+        if (t + S - 1 < nsteps) issue(t + S - 1);              // overwrites stage t-1 (all waves are past it)
+#endif
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int row = m0 + wm + i * 16 + lg + 4 * r;
-                if (row < M && col < N && (!mirror || row >= col)) {
-                    const size_t o = size_t(row) * N + col;
-                    double sum = 0.0;
-                    for (int z = 0; z < int(gridDim.z); ++z)
-                        sum += (z == int(blockIdx.z)) ? acc[i][j][r]
-                                                      : __hip_atomic_load(&slab[(size_t(bz) * gridDim.z + z) * MN + o], __ATOMIC_RELAXED,
-                                                                          __HIP_MEMORY_SCOPE_AGENT);
-                    C[o] = alpha * sum;
-                    if (mirror) C[size_t(col) * N + row] = alpha * sum;
-                }
-            }
+        for (int q = 0; q < NQ; ++q) {
+            if (q + 1 < NQ) frag(q + 1, af[(q + 1) & 1], bf[(q + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);   // keep those reads ahead of this substep's MFMAs
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc2[q % NACC][i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[q & 1][i], bf[q & 1][j], acc2[q % NACC][i][j], 0, 0, 0);
         }
+    }
+    __syncthreads();   // every wave is done with the stages before the epilogue reuses the LDS
+    gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, lds, ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
+    XRS_TRACE_END
 }
 
 template <class PTR>
@@ -395,10 +656,117 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
     check_launch("k_gemm_f64");
 }
 
+template <int BM, int BN, int WGM, int WGN, int WGK, class PTR>
+static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, bool ta, size_t ldb, bool tb, int M, int N,
+                        int K, int splits, int kps, double alpha, double* slab, int* tickets, int sym) {
+    const int tiles_m = M / BM, tiles_n = N / BN;
+    // symmetric: only the lower tiles are launched (the kernel maps x to (tm >= tn)), so the workgroups of
+    // every split spread evenly over the XCDs
+    dim3 grid(unsigned(sym ? tiles_m * (tiles_m + 1) / 2 : tiles_m * tiles_n), unsigned(count), unsigned(splits));
+    int xg = 0;
+    if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
+    else xg = (tiles_m % 8 == 0) ? 2 : 0;
+    KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * double(K),
+                      count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
+#define XRS_GLDS_LAUNCH(TA_, TB_)                                                                              \
+    hipLaunchKernelGGL((k_gemm_glds<BM, BN, WGM, WGN, WGK, TA_, TB_, PTR>), grid, dim3(WGM * WGN * WGK * 64), 0, \
+                       h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets, sym)
+    if (!ta && !tb) XRS_GLDS_LAUNCH(false, false);
+    else if (!ta && tb) XRS_GLDS_LAUNCH(false, true);
+    else if (ta && !tb) XRS_GLDS_LAUNCH(true, false);
+    else XRS_GLDS_LAUNCH(true, true);
+#undef XRS_GLDS_LAUNCH
+    check_launch("k_gemm_glds");
+}
+
+// The LDS-DMA pipeline (k_gemm_glds) for whole-tile shapes with 16-B aligned operands; false = not taken
+// (the caller runs the general kernel). Tiles: g1 64x80 (4 waves, 16x80 each), g2 80x64 (4 waves, 80x16 each), g3 64x64
+// (4 waves, 32x32), g4 64x64 (8 waves, K-substeps split over 2 wave groups), g5 32x32 (4 waves), g6 / g7 the
+// 64x80 / 80x64 tiles with 8 waves (K-substeps split over 2 wave groups); g8 / g9 the same tiles with 4
+// waves of 32x80 / 80x32 (2 wave groups); g10 64x64 with 4 waves of 64x64 (4 wave groups); g11 64x64 with 4
+// waves of 32x64 (2 wave groups).
+// XRS_GEMM_GLDS="v,target": v = 0 off, 1-5 forced variant, -1 automatic; target = workgroups aimed at
+// by the split-K choice.
+template <class PTR>
+static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int K, double alpha, size_t lda, bool ta,
+                      size_t ldb, bool tb, bool sym) {
+    static int g_var = -1, g_target = 256;
+    static bool read = false;
+    if (!read) {
+        read = true;
+        if (const char* e = std::getenv("XRS_GEMM_GLDS")) std::sscanf(e, "%d,%d", &g_var, &g_target);
+    }
+    if (g_var == 0) return false;
+    if (K % kGldsBK != 0 || (lda & 1) || (ldb & 1)) return false;
+    for (int i = 0; i < count; ++i)
+        if ((reinterpret_cast<uintptr_t>(P.a(i)) & 15) || (reinterpret_cast<uintptr_t>(P.b(i)) & 15)) return false;
+    const int bms[12] = {0, 64, 80, 64, 64, 32, 64, 80, 64, 80, 64, 64},
+              bns[12] = {0, 80, 64, 64, 64, 32, 80, 64, 80, 64, 64, 64};
+    auto fits = [&](int v) { return M % bms[v] == 0 && N % bns[v] == 0 && (!sym || bms[v] == bns[v]); };
+    auto ntiles = [&](int v) {
+        const long tm = M / bms[v], tn = N / bns[v];
+        return sym ? long(count) * tm * (tm + 1) / 2 : long(count) * tm * tn;
+    };
+    int var = g_var;
+    if (var < 0) {
+        // measured on the TT shapes (tools/gemm_tt_bench.py, back-to-back wall per call): 256x5120x256 NN/TN
+        // g6 18.7-20.2 us, g1 19.6-19.9, g8 20.0-20.3 (old kernel 24.5-25.1); 5120x256x256 g7 19.0-19.2, g2
+        // 19.4; Grams 256^2 x 5120 g4 22.3-23.7, g3 23.4-25.2, g11 24.3-24.6 (old 25.5-28.0); 512x10240x512
+        // and 512^2 x 10240: g4 117.8-125 (old 126-128)
+        var = 0;
+        if (sym) {
+            if (fits(4)) var = 4;
+            else if (fits(5)) var = 5;
+        } else if (fits(6) && ntiles(6) >= 192) var = 6;
+        else if (fits(7) && ntiles(7) >= 192) var = 7;
+        else if (fits(4)) var = 4;
+        else if (fits(5)) var = 5;
+        if (var == 0) return false;
+    }
+    if (var < 1 || var > 11 || !fits(var)) return false;
+    // split-K: whole 32-deep steps per slice, aiming at `target` workgroups
+    const long tiles = ntiles(var);
+    const int ksteps = K / kGldsBK;
+    int splits = 1;
+    if (tiles < g_target) splits = int(std::min<long>((g_target + tiles - 1) / tiles, std::max(1, ksteps / 4)));
+    int kps = (ksteps + splits - 1) / splits * kGldsBK;
+    splits = (K + kps - 1) / kps;
+    DevBuf slab;
+    if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
+    const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= 65536 && bms[var] * bns[var] <= 4096;
+    const long grid_tiles = long(count) * (M / bms[var]) * (N / bns[var]);
+    int* tickets = (splits > 1 && small_slab && grid_tiles <= xrs_handle_s::kTicketCap) ? h->tickets : nullptr;
+#define XRS_GLDS(...) launch_glds<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets, sym ? 1 : 0)
+    switch (var) {
+        case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
+        case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
+        case 3: XRS_GLDS(64, 64, 2, 2, 1); break;
+        case 4: XRS_GLDS(64, 64, 2, 2, 2); break;
+        case 6: XRS_GLDS(64, 80, 4, 1, 2); break;
+        case 7: XRS_GLDS(80, 64, 1, 4, 2); break;
+        case 8: XRS_GLDS(64, 80, 2, 1, 2); break;
+        case 9: XRS_GLDS(80, 64, 1, 2, 2); break;
+        case 10: XRS_GLDS(64, 64, 1, 1, 4); break;
+        case 11: XRS_GLDS(64, 64, 2, 1, 2); break;
+        default: XRS_GLDS(32, 32, 2, 2, 1); break;
+    }
+#undef XRS_GLDS
+    if (splits > 1 && tickets == nullptr) {
+        const size_t MN = size_t(M) * N;
+        const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
+        KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
+        hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab.d(), MN,
+                           splits, alpha, sym ? N : 0);
+        check_launch("k_splitk_reduce");
+    }
+    return true;
+}
+
 template <class PTR>
 static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t Ns, double alpha, size_t lda, bool ta,
                       size_t Ks, size_t ldb, bool tb, bool sym = false) {
     const int M = int(Ms), N = int(Ns), K = int(Ks);
+    if (gemm_glds(h, P, count, M, N, K, alpha, lda, ta, ldb, tb, sym)) return;
     // Tile choice (XRS_GEMM_CFG="variant,kmin,target" overrides for tuning experiments):
     //   v1 128x128 (8 waves 2x4)              large problems
     //   v2  64x64  (8 waves 2x4)              mid-size
@@ -570,6 +938,16 @@ void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t
 }
 
 }  // namespace xrs
+
+#ifdef XRS_GEMM_TRACE
+extern "C" int xrs_debug_gemm_trace(void* buf, void* steps) {
+    unsigned long long* p = static_cast<unsigned long long*>(buf);
+    unsigned long long* q = static_cast<unsigned long long*>(steps);
+    return hipMemcpyToSymbol(HIP_SYMBOL(xrs::g_gemm_trace), &p, sizeof(p)) == hipSuccess &&
+                   hipMemcpyToSymbol(HIP_SYMBOL(xrs::g_gemm_steps), &q, sizeof(q)) == hipSuccess
+               ? 0 : 1;
+}
+#endif
 
 extern "C" int xrs_gemm(xrs_handle_t h, double* C, size_t M, size_t N, double alpha, const double* A, size_t lda,
                         int transA, size_t K, const double* B, size_t ldb, int transB) {
