@@ -182,6 +182,18 @@ int xrs_tt_dot(xrs_handle_t handle, double* result, size_t d, const size_t* n,
                const size_t* rx, const double* const* xcores,
                const size_t* ry, const double* const* ycores);
 
+/** Asynchronous <x,y> (same algorithm and result as xrs_tt_dot): enqueued on the handle's side streams
+ *  1 and 2 from the main stream's current point, NOT joined into the main stream, so work enqueued next
+ *  (e.g. xrs_tt_round of x) runs beside it. Until xrs_tt_dot_wait, the cores may be read and released
+ *  (releases through this handle -- xrs_free, a round replacing cores -- wait for the inner product
+ *  first) but not written in place. One in flight per handle. No counterpart in the reference (whose
+ *  value_t(x(i&0)*y(i&0)) is synchronous); xrs_tt_dot_wait returns what xrs_tt_dot would have. */
+int xrs_tt_dot_async(xrs_handle_t handle, size_t d, const size_t* n,
+                     const size_t* rx, const double* const* xcores,
+                     const size_t* ry, const double* const* ycores);
+/** Waits for the handle's asynchronous inner product; *result on host. */
+int xrs_tt_dot_wait(xrs_handle_t handle, double* result);
+
 /** All-reduce (element-wise sum over all ranks) of `count` doubles at the device pointer `buf`, in place.
  *  Called by the sharded TT entry points with the handle's stream synchronised; returns 0 on success.
  *  The Python layer (xerus_amd.dist) binds it to torch.distributed (RCCL over xGMI on MI355X).

@@ -47,6 +47,50 @@ def test_dot(handle, ref, dims, ranks):
     nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
     assert abs(d_gpu - d_ref) <= 1e-12 * nx * ny
     assert abs(gx.dot(gx) - nx * nx) <= 1e-12 * nx * nx
+    # the asynchronous form runs the same two-ended zipper on the side streams: bitwise the same value
+    # from order 4 on (below, the synchronous form is one-ended)
+    d_async = gx.dot_async(gy).result()
+    assert d_async == d_gpu if len(dims) >= 4 else abs(d_async - d_ref) <= 1e-12 * nx * ny
+
+
+@pytest.mark.parametrize("dims,ranks", [
+    ([4, 5, 3, 4, 2], [3, 6, 5, 2]),
+    ([7, 3, 5], [6, 4]),
+    ([5, 6], [4]),
+    ([20] * 10, [128] * 9),
+])
+def test_dot_async_beside_round(handle, ref, dims, ranks):
+    """x.dot_async(y) overlapped with x.round (which replaces x's cores): the inner product is the one of
+    the pre-round x (the round's releases wait for it), the round is unaffected, and the handle accepts
+    the next async call only after the wait."""
+    rng = ref.Rng(11)
+    x = ref.TT.random_raw(dims, ranks, rng)
+    y = ref.TT.random_raw(dims, ranks, rng)
+    gx = capi.TTDevice.from_cores(handle, x.cores)
+    gy = capi.TTDevice.from_cores(handle, y.cores)
+    d_seq = gx.dot(gy)
+    nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
+    assert abs(d_seq - ref.dot(x, y)) <= 1e-12 * nx * ny
+    target = max(1, max(ranks) // 2)
+    for _ in range(3):
+        fut = gx.dot_async(gy)
+        with pytest.raises(capi.XrsError):
+            gx.dot_async(gy)   # one in flight per handle
+        before = [c.copy() for c in gx.cores()] if _ == 0 else None
+        gx.round(target)
+        d = fut.result()
+        if _ == 0:
+            assert d == d_seq if len(dims) >= 4 else abs(d - d_seq) <= 1e-13 * nx * ny
+            ox = ref.TT([c.copy() for c in before])
+            ox.round(target)
+            assert gx.r == [1] + list(ox.ranks) + [1]
+            e_ref, nrm = _tt_diff_norm(ref, ox.cores, before)
+            e_gpu, _ = _tt_diff_norm(ref, gx.cores(), before)
+            assert abs(e_gpu - e_ref) <= 1e-6 * nrm
+        # next iteration: <x_rounded, y> against the synchronous zipper on the same cores
+        assert abs(gx.dot_async(gy).result() - gx.dot(gy)) <= 1e-13 * nx * ny
+    with pytest.raises(capi.XrsError):
+        capi._check("xrs_tt_dot_wait", handle.lib.xrs_tt_dot_wait(handle.h, capi.C.byref(capi.C.c_double())))
 
 
 @pytest.mark.parametrize("dims,ranks", [([4, 5, 3, 4, 2], [3, 6, 5, 2]), ([3, 3, 3, 3], [9, 9, 9]),
@@ -282,3 +326,35 @@ def test_round_ranks_above_512(handle, ref, n, ranks):
     e_ref, _ = _tt_diff_norm(ref, y.cores, x.cores)
     e_gpu, _ = _tt_diff_norm(ref, g2.cores(), x.cores)
     assert abs(e_gpu - e_ref) <= 1e-6 * nrm
+
+
+def test_paired_chain_launches(handle, ref, monkeypatch):
+    """XRS_GEMM_PAIR=1: both chains of the round and both ends of <x,y> as paired launches (k_gemm_glds2,
+    two shapes / transposes per grid) -- same results as the two-stream form within rounding."""
+    dims, ranks = [20] * 7, [20, 256, 256, 256, 256, 20]
+    rng = ref.Rng(21)
+    x = ref.TT.random_raw(dims, ranks, rng)
+    y = ref.TT.random_raw(dims, ranks, rng)
+    nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
+    d_ref = ref.dot(x, y)
+    ox = x.copy()
+    ox.move_core(0)
+    ox.round(256)
+    results = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("XRS_GEMM_PAIR", mode)
+        gx = capi.TTDevice.from_cores(handle, x.cores)
+        gy = capi.TTDevice.from_cores(handle, y.cores)
+        d = gx.dot(gy)
+        assert abs(d - d_ref) <= 1e-12 * nx * ny
+        assert abs(gx.dot_async(gy).result() - d_ref) <= 1e-12 * nx * ny
+        gx.move_core(0)
+        gx.round(256)
+        assert handle.last_round_path() == "chain"
+        assert gx.r == [1] + list(ox.ranks) + [1]
+        diff, nrm = _tt_diff_norm(ref, gx.cores(), ox.cores)
+        assert diff <= 1e-10 * nrm
+        results[mode] = d
+        gx.free()
+        gy.free()
+    assert abs(results["0"] - results["1"]) <= 1e-13 * nx * ny

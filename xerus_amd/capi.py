@@ -60,6 +60,9 @@ SIGNATURES = {
                                C.POINTER(_SZ), C.c_double]),
     "xrs_tt_dot": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                              C.POINTER(_SZ), C.POINTER(_DP)]),
+    "xrs_tt_dot_async": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
+                                   C.POINTER(_DP)]),
+    "xrs_tt_dot_wait": (C.c_int, [_DP, C.POINTER(C.c_double)]),
     "xrs_tt_round_sharded": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
                                        C.c_double, _DP, _DP, C.POINTER(C.c_int)]),
     "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
@@ -358,6 +361,21 @@ class DeviceArray:
             pass
 
 
+class DotFuture:
+    """Result of TTDevice.dot_async."""
+
+    def __init__(self, handle: Handle):
+        self.handle = handle
+        self._value = None
+
+    def result(self) -> float:
+        if self._value is None:
+            out = C.c_double()
+            _check("xrs_tt_dot_wait", self.handle.lib.xrs_tt_dot_wait(self.handle.h, C.byref(out)))
+            self._value = out.value
+        return self._value
+
+
 class TTDevice:
     """A TT tensor whose cores live in the handle's device pool (core k: (r[k], n[k], r[k+1]) row-major).
 
@@ -463,6 +481,18 @@ class TTDevice:
         _, ry, yc = other._arrays()
         _check("xrs_tt_dot", self.handle.lib.xrs_tt_dot(self.handle.h, C.byref(out), self.order, n, rx, xc, ry, yc))
         return out.value
+
+    def dot_async(self, other: "TTDevice") -> "DotFuture":
+        """<self, other> enqueued on the handle's side streams (xrs_tt_dot_async): work enqueued next on the
+        handle's main stream (e.g. self.round) runs beside it; DotFuture.result() waits."""
+        if self.dims != other.dims:
+            raise ValueError(f"dot of TTs with different dimensions: {self.dims} vs {other.dims}")
+        if other.handle is not self.handle:
+            raise ValueError("dot_async: both TTs must live on the same handle")
+        n, rx, xc = self._arrays()
+        _, ry, yc = other._arrays()
+        _check("xrs_tt_dot_async", self.handle.lib.xrs_tt_dot_async(self.handle.h, self.order, n, rx, xc, ry, yc))
+        return DotFuture(self.handle)
 
     def frob_norm(self) -> float:
         if self.canonicalized:

@@ -55,9 +55,10 @@ __global__ void __launch_bounds__(RB) k_reduce_final(const double* __restrict__ 
     if (threadIdx.x == 0) out[0] = take_sqrt ? sqrt(s) : s;
 }
 
-void reduce_to_device(xrs_handle_t h, int mode, const double* x, const double* y, size_t n, double* out_dev) {
+void reduce_to_device(xrs_handle_t h, int mode, const double* x, const double* y, size_t n, double* out_dev,
+                      double* partial) {
     KernelTimer timer(h, XRS_KFAM_ELEMWISE, 2.0 * double(n), double(mode == 1 ? 2 : 1) * 8.0 * double(n));
-    double* partial = static_cast<double*>(h->dev_scratch) + 64;
+    if (partial == nullptr) partial = static_cast<double*>(h->dev_scratch) + 64;
     const int nb = int(std::max<size_t>(1, std::min<size_t>(RMAXB, (n + RB * 4 - 1) / (RB * 4))));
     if (mode == 0) hipLaunchKernelGGL(k_reduce_partial<0>, dim3(nb), dim3(RB), 0, h->stream, x, y, n, partial);
     else if (mode == 1) hipLaunchKernelGGL(k_reduce_partial<1>, dim3(nb), dim3(RB), 0, h->stream, x, y, n, partial);

@@ -464,16 +464,26 @@ struct GldsImg {
 template <int BM, int BN, int WGM, int WGN, int WGK>
 constexpr int glds_min_waves() { return (WGM * WGN * WGK * 64 >= 512) ? 2 : 1; }
 
+// LDS of the glds pipeline: S = 3 stages of the A and B images
+template <int BM, int BN>
+constexpr int glds_lds_doubles() { return 3 * (BM + BN) * kGldsBK; }
+
+// One output tile of the glds pipeline for entry blockIdx.y of `ptrs` (tile blockIdx.x, K-slice
+// blockIdx.z); `lds` holds glds_lds_doubles<BM, BN>() doubles. Shared by k_gemm_glds (one shape per
+// launch) and k_gemm_glds2 (two entries of different shapes / transposes in one launch).
 template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR>
-__global__ void __launch_bounds__(WGM * WGN * WGK * 64, (glds_min_waves<BM, BN, WGM, WGN, WGK>()))
-k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
-            double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym) {
-    XRS_TRACE_BEGIN
+__device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& ptrs, size_t lda, size_t ldb, int M, int N,
+                                          int K, int kps, double alpha, double* __restrict__ slab, int tiles_m,
+                                          int xcd_group, int* __restrict__ tickets, int sym, int tri) {
+#ifdef XRS_GEMM_TRACE
+    const unsigned long long xrs_c0 = __builtin_amdgcn_s_memtime();
+#endif
     constexpr int BK = kGldsBK, S = 3;
     constexpr int NW = WGM * WGN * WGK;
     using IA = GldsImg<BM, TA>;   // A stored [m][k] (RK) or, transposed, [k][m] (KR)
     using IB = GldsImg<BN, !TB>;  // B stored [k][n] (KR) or, transposed, [n][k] (RK)
     constexpr int STAGE = IA::DOUBLES + IB::DOUBLES;
+    static_assert(S * STAGE == glds_lds_doubles<BM, BN>(), "LDS layout");
     constexpr int INSTR = IA::INSTR + IB::INSTR;
     // wave w issues DMA instructions j = w, w + NW, ...: PER_WAVE of them, or one fewer for w >= INSTR % NW
     constexpr int PER_WAVE = (INSTR + NW - 1) / NW;
@@ -484,7 +494,6 @@ k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps
     static_assert(BK % (4 * WGK) == 0, "K-step must split evenly over the wave groups");
     constexpr int NACC = (TM * TN <= 2) ? 2 : 1;
     static_assert(WGK == 1 || (WGK - 1) * WGM * WGN * TM * TN * 256 <= S * STAGE, "LDS reduction buffer too small");
-    __shared__ double lds[S * STAGE];   // the one LDS array (trap 4a: no second __shared__ object)
 
     const int bz = blockIdx.y;
     const double* __restrict__ A = ptrs.a(bz);
@@ -515,8 +524,12 @@ k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps
         }
     }
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kbeg = blockIdx.z * kps;
-    const int nsteps = max(0, min(K, kbeg + kps) - kbeg) / BK;   // (the host guarantees whole steps)
+    // triangular operands (exact zeros outside the triangle): op(A) lower (bit 0) needs k < m0 + BM only,
+    // op(B) lower (bit 1) k >= n0 only -- whole K-steps of the slice's range
+    const int klo = (tri & 2) ? (n0 / BK) * BK : 0;
+    const int khi = (tri & 1) ? min(K, (m0 + BM + BK - 1) / BK * BK) : K;
+    const int kbeg = max(int(blockIdx.z) * kps, klo);
+    const int nsteps = max(0, min(khi, int(blockIdx.z) * kps + kps) - kbeg) / BK;   // (the host guarantees whole steps)
     const bool full = wave < INSTR % NW || INSTR % NW == 0;     // issues PER_WAVE DMAs per stage (else one fewer)
 
     // this wave's DMA instructions: j = wave + NW u; j < IA::INSTR -> A image, else B image
@@ -599,7 +612,48 @@ k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps
     }
     __syncthreads();   // every wave is done with the stages before the epilogue reuses the LDS
     gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, lds, ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
+}
+
+template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR>
+__global__ void __launch_bounds__(WGM * WGN * WGK * 64, (glds_min_waves<BM, BN, WGM, WGN, WGK>()))
+k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
+            double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym, int tri) {
+    XRS_TRACE_BEGIN
+    __shared__ double lds[glds_lds_doubles<BM, BN>()];   // the one LDS array (trap 4a: no second __shared__ object)
+    glds_body<BM, BN, WGM, WGN, WGK, TA, TB, PTR>(lds, ptrs, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xcd_group,
+                                                  tickets, sym, tri);
     XRS_TRACE_END
+}
+
+// Two GEMMs of different shapes and transposes in ONE launch (blockIdx.y = entry, each entry with its own
+// tile configuration; both configurations have the same wave count and the same number of tiles): the
+// two concurrent chains of a TT round / inner product step as one grid instead of two kernels sharing
+// the chip from two streams.
+struct GemmPair {
+    const double* A[2];
+    const double* B[2];
+    double* C[2];
+    size_t lda[2], ldb[2];
+    int M[2], N[2], tiles_m[2], xg[2];
+    __host__ __device__ const double* a(int i) const { return A[i]; }
+    __host__ __device__ const double* b(int i) const { return B[i]; }
+    __device__ double* c(int i) const { return C[i]; }
+};
+
+template <int BM0, int BN0, int WGM0, int WGN0, int WGK0, bool TA0, bool TB0,
+          int BM1, int BN1, int WGM1, int WGN1, int WGK1, bool TA1, bool TB1>
+__global__ void __launch_bounds__(WGM0 * WGN0 * WGK0 * 64, (glds_min_waves<BM0, BN0, WGM0, WGN0, WGK0>()))
+k_gemm_glds2(const GemmPair P, int K, int kps, double alpha, double* __restrict__ slab, int* __restrict__ tickets,
+             int sym) {
+    static_assert(WGM0 * WGN0 * WGK0 == WGM1 * WGN1 * WGK1, "both entries need the same wave count");
+    constexpr int L0 = glds_lds_doubles<BM0, BN0>(), L1 = glds_lds_doubles<BM1, BN1>();
+    __shared__ double lds[L0 > L1 ? L0 : L1];
+    if (blockIdx.y == 0)
+        glds_body<BM0, BN0, WGM0, WGN0, WGK0, TA0, TB0, GemmPair>(lds, P, P.lda[0], P.ldb[0], P.M[0], P.N[0], K, kps, alpha,
+                                                                slab, P.tiles_m[0], P.xg[0], tickets, sym, 0);
+    else
+        glds_body<BM1, BN1, WGM1, WGN1, WGK1, TA1, TB1, GemmPair>(lds, P, P.lda[1], P.ldb[1], P.M[1], P.N[1], K, kps, alpha,
+                                                                slab, P.tiles_m[1], P.xg[1], tickets, sym, 0);
 }
 
 template <class PTR>
@@ -658,7 +712,7 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
 
 template <int BM, int BN, int WGM, int WGN, int WGK, class PTR>
 static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, bool ta, size_t ldb, bool tb, int M, int N,
-                        int K, int splits, int kps, double alpha, double* slab, int* tickets, int sym) {
+                        int K, int splits, int kps, double alpha, double* slab, int* tickets, int sym, int tri) {
     const int tiles_m = M / BM, tiles_n = N / BN;
     // symmetric: only the lower tiles are launched (the kernel maps x to (tm >= tn)), so the workgroups of
     // every split spread evenly over the XCDs
@@ -666,11 +720,22 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
-    KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * double(K),
+    // executed K-depth summed over the tile rows / columns (triangular operands skip their zero blocks)
+    double kdepth = double(K);
+    if (tri & 1) {
+        double s = 0;
+        for (int m0 = 0; m0 < M; m0 += BM) s += std::min(K, (m0 + BM + kGldsBK - 1) / kGldsBK * kGldsBK);
+        kdepth = s / tiles_m;
+    } else if (tri & 2) {
+        double s = 0;
+        for (int n0 = 0; n0 < N; n0 += BN) s += K - (n0 / kGldsBK) * kGldsBK;
+        kdepth = s / tiles_n;
+    }
+    KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * kdepth,
                       count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GLDS_LAUNCH(TA_, TB_)                                                                              \
     hipLaunchKernelGGL((k_gemm_glds<BM, BN, WGM, WGN, WGK, TA_, TB_, PTR>), grid, dim3(WGM * WGN * WGK * 64), 0, \
-                       h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets, sym)
+                       h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets, sym, tri)
     if (!ta && !tb) XRS_GLDS_LAUNCH(false, false);
     else if (!ta && tb) XRS_GLDS_LAUNCH(false, true);
     else if (ta && !tb) XRS_GLDS_LAUNCH(true, false);
@@ -689,7 +754,7 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
 // by the split-K choice.
 template <class PTR>
 static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int K, double alpha, size_t lda, bool ta,
-                      size_t ldb, bool tb, bool sym) {
+                      size_t ldb, bool tb, bool sym, int tri) {
     static int g_var = -1, g_target = 256;
     static bool read = false;
     if (!read) {
@@ -736,7 +801,7 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
     const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= 65536 && bms[var] * bns[var] <= 4096;
     const long grid_tiles = long(count) * (M / bms[var]) * (N / bns[var]);
     int* tickets = (splits > 1 && small_slab && grid_tiles <= xrs_handle_s::kTicketCap) ? h->tickets : nullptr;
-#define XRS_GLDS(...) launch_glds<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets, sym ? 1 : 0)
+#define XRS_GLDS(...) launch_glds<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets, sym ? 1 : 0, tri)
     switch (var) {
         case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
         case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
@@ -764,9 +829,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
 
 template <class PTR>
 static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t Ns, double alpha, size_t lda, bool ta,
-                      size_t Ks, size_t ldb, bool tb, bool sym = false) {
+                      size_t Ks, size_t ldb, bool tb, bool sym = false, int tri = 0) {
     const int M = int(Ms), N = int(Ns), K = int(Ks);
-    if (gemm_glds(h, P, count, M, N, K, alpha, lda, ta, ldb, tb, sym)) return;
+    if (gemm_glds(h, P, count, M, N, K, alpha, lda, ta, ldb, tb, sym, tri)) return;   // (the general kernel ignores tri)
     // Tile choice (XRS_GEMM_CFG="variant,kmin,target" overrides for tuning experiments):
     //   v1 128x128 (8 waves 2x4)              large problems
     //   v2  64x64  (8 waves 2x4)              mid-size
@@ -895,14 +960,14 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
 }
 
 void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const double* A, size_t lda, bool ta, size_t Ks,
-          const double* B, size_t ldb, bool tb) {
+          const double* B, size_t ldb, bool tb, int tri) {
     if (Ms == 0 || Ns == 0) return;
     XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
     if (Ks == 0) {
         XRS_HIP(hipMemsetAsync(C, 0, Ms * Ns * 8, h->stream));
         return;
     }
-    gemm_impl(h, GemmOne{A, B, C}, 1, Ms, Ns, alpha, lda, ta, Ks, ldb, tb);
+    gemm_impl(h, GemmOne{A, B, C}, 1, Ms, Ns, alpha, lda, ta, Ks, ldb, tb, false, tri);
 }
 
 void gemm_sym(xrs_handle_t h, double* C, size_t Ns, double alpha, const double* A, size_t lda, bool ta, size_t Ks,
@@ -917,7 +982,7 @@ void gemm_sym(xrs_handle_t h, double* C, size_t Ns, double alpha, const double* 
 }
 
 void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t Ns, double alpha, const double* const* A,
-                  size_t lda, bool ta, size_t Ks, const double* const* B, size_t ldb, bool tb, bool sym) {
+                  size_t lda, bool ta, size_t Ks, const double* const* B, size_t ldb, bool tb, bool sym, int tri) {
     XRS_REQUIRE(!sym || Ms == Ns, "symmetric batch needs square results");
     if (Ms == 0 || Ns == 0 || count <= 0) return;
     XRS_REQUIRE(Ms < (1u << 30) && Ns < (1u << 30) && Ks < (1u << 30), "GEMM dimension too large");
@@ -933,8 +998,105 @@ void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t
             P.B[i] = B[b0 + i];
             P.C[i] = C[b0 + i];
         }
-        gemm_impl(h, P, c, Ms, Ns, alpha, lda, ta, Ks, ldb, tb, sym);
+        gemm_impl(h, P, c, Ms, Ns, alpha, lda, ta, Ks, ldb, tb, sym, tri);
     }
+}
+
+// Two independent GEMMs in one k_gemm_glds2 launch (see GemmPair). Taken when both are glds-eligible
+// (whole 32-deep K-steps, 16-B aligned operands, even leading dimensions), share K (and the result
+// size when split-K applies), and their transposes and shapes match an instantiated configuration:
+//   (NN, NN) and (TN, NN): 64x80 / 80x64 tiles (the T = G M / M H products of the chains, 256 tiles each
+//   at r = 256, n = 20); (TN, NT): 64x64 tiles (the chains' Grams M^T T / M T^T, symmetric or not).
+// false: nothing launched (the caller runs the two GEMMs separately).
+bool gemm_pair(xrs_handle_t h, const GemmSpec& g0, const GemmSpec& g1, bool sym, bool dry) {
+    // opt-in (XRS_GEMM_PAIR=1, read per call): measured slower than the two chains on two streams, where
+    // one chain's split-K reduce and boundary products overlap the other chain's GEMMs
+    const char* on = std::getenv("XRS_GEMM_PAIR");
+    if (on == nullptr || on[0] == '0' || g0.K != g1.K || g0.K == 0 || g0.K % kGldsBK != 0) return false;
+    const GemmSpec* g[2] = {&g0, &g1};
+    for (const GemmSpec* e : g) {
+        if ((e->lda & 1) || (e->ldb & 1) || (reinterpret_cast<uintptr_t>(e->A) & 15) || (reinterpret_cast<uintptr_t>(e->B) & 15))
+            return false;
+        if (e->M >= (1u << 30) || e->N >= (1u << 30) || e->K >= (1u << 30)) return false;
+    }
+    const int K = int(g0.K);
+    auto fits = [&](const GemmSpec& e, int bm, int bn) { return e.M % bm == 0 && e.N % bn == 0; };
+    // configuration: 0 = 64x80 (4,1,2), 1 = 80x64 (1,4,2), 2 = 64x64 (2,2,2)
+    int cfg[2];
+    const int bms[3] = {64, 80, 64}, bns[3] = {80, 64, 64};
+    for (int i = 0; i < 2; ++i) {
+        const GemmSpec& e = *g[i];
+        if (sym) cfg[i] = (e.M == e.N && fits(e, 64, 64)) ? 2 : -1;
+        else if (!(g0.ta && !g0.tb && !g1.ta && g1.tb) && fits(e, 64, 80)) cfg[i] = 0;
+        else if (!(g0.ta && !g0.tb && !g1.ta && g1.tb) && fits(e, 80, 64)) cfg[i] = 1;
+        else cfg[i] = fits(e, 64, 64) ? 2 : -1;
+        if (cfg[i] < 0) return false;
+    }
+    auto tiles = [&](int i) -> long {
+        const long tm = long(g[i]->M) / bms[cfg[i]], tn = long(g[i]->N) / bns[cfg[i]];
+        return sym ? tm * (tm + 1) / 2 : tm * tn;
+    };
+    if (tiles(0) != tiles(1)) return false;
+    // instantiated transpose / configuration combinations
+    const bool nn_nn = !g0.ta && !g0.tb && !g1.ta && !g1.tb;
+    const bool tn_nn = g0.ta && !g0.tb && !g1.ta && !g1.tb;
+    const bool tn_nt = g0.ta && !g0.tb && !g1.ta && g1.tb;
+    int kind = -1;
+    if ((nn_nn || tn_nn) && cfg[0] == 0 && cfg[1] == 1) kind = nn_nn ? 0 : 1;
+    else if (tn_nt && cfg[0] == 2 && cfg[1] == 2) kind = 2;
+    if (kind < 0) return false;
+    // split-K toward 256 workgroups in all, whole 32-deep steps per slice
+    const long t = 2 * tiles(0);
+    const int ksteps = K / kGldsBK;
+    int splits = 1;
+    if (t < 256) splits = int(std::min<long>((256 + t - 1) / t, std::max(1, ksteps / 4)));
+    int kps = (ksteps + splits - 1) / splits * kGldsBK;
+    splits = (K + kps - 1) / kps;
+    if (splits > 1 && g0.M * g0.N != g1.M * g1.N) return false;   // (slab layout: equal result sizes)
+    if (dry) return true;
+    GemmPair P{};
+    for (int i = 0; i < 2; ++i) {
+        const GemmSpec& e = *g[i];
+        P.A[i] = e.A;
+        P.B[i] = e.B;
+        P.C[i] = e.C;
+        P.lda[i] = e.lda;
+        P.ldb[i] = e.ldb;
+        P.M[i] = int(e.M);
+        P.N[i] = int(e.N);
+        P.tiles_m[i] = int(e.M) / bms[cfg[i]];
+        const int tn = int(e.N) / bns[cfg[i]];
+        P.xg[i] = sym ? 0 : (e.N >= e.M ? ((tn % 8 == 0) ? 1 : 0) : ((P.tiles_m[i] % 8 == 0) ? 2 : 0));
+    }
+    const size_t MN = g0.M * g0.N;
+    DevBuf slab;
+    if (splits > 1) slab = DevBuf(h, 2 * size_t(splits) * MN * sizeof(double));
+    // in-launch combine for small per-tile slabs (as gemm_glds)
+    const bool small_slab = size_t(splits) * 64 * 64 * sizeof(double) <= 65536;
+    int* tickets = (splits > 1 && kind == 2 && small_slab && 2 * tiles(0) <= xrs_handle_s::kTicketCap) ? h->tickets : nullptr;
+    KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * (double(g0.M) * g0.N + double(g1.M) * g1.N) * K,
+                      8.0 * (double(g0.M) * K + double(K) * g0.N + double(g1.M) * K + double(K) * g1.N +
+                             (double(g0.M) * g0.N + double(g1.M) * g1.N) * splits));
+    const dim3 grid(unsigned(tiles(0)), 2u, unsigned(splits));
+    const int symf = sym ? 1 : 0;
+    if (kind == 0)
+        hipLaunchKernelGGL((k_gemm_glds2<64, 80, 4, 1, 2, false, false, 80, 64, 1, 4, 2, false, false>), grid, dim3(512), 0,
+                           h->stream, P, K, kps, 1.0, slab.d(), tickets, symf);
+    else if (kind == 1)
+        hipLaunchKernelGGL((k_gemm_glds2<64, 80, 4, 1, 2, true, false, 80, 64, 1, 4, 2, false, false>), grid, dim3(512), 0,
+                           h->stream, P, K, kps, 1.0, slab.d(), tickets, symf);
+    else
+        hipLaunchKernelGGL((k_gemm_glds2<64, 64, 2, 2, 2, true, false, 64, 64, 2, 2, 2, false, true>), grid, dim3(512), 0,
+                           h->stream, P, K, kps, 1.0, slab.d(), tickets, symf);
+    check_launch("k_gemm_glds2");
+    if (splits > 1 && tickets == nullptr) {
+        const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
+        KernelTimer t2(h, XRS_KFAM_ELEMWISE, 2.0 * double(MN) * splits, 2 * 8.0 * double(MN) * (splits + 1));
+        hipLaunchKernelGGL(k_splitk_reduce<GemmPair>, dim3(blocks, 2u), dim3(256), 0, h->stream, P, slab.d(), MN, splits,
+                           1.0, sym ? int(g0.N) : 0);
+        check_launch("k_splitk_reduce");
+    }
+    return true;
 }
 
 }  // namespace xrs

@@ -113,6 +113,15 @@ void host_wait(xrs_handle_t h) {
     XRS_HIP(e);
 }
 
+void fence_readers(xrs_handle_t h) {
+    if (!h->reader_pending) return;
+    // the worker thread has synchronised the product's streams when it reports done: afterwards no
+    // device work reads the handle's blocks any more (a host wait, normally already satisfied: the
+    // round releases x's old cores after its own check synchronisation)
+    wait_dot_done(h);
+    h->reader_pending = false;
+}
+
 void check_launch(const char* what) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) throw Error{XRS_EHIP, std::string(what) + ": " + hipGetErrorString(e)};
@@ -200,6 +209,8 @@ StreamFork::~StreamFork() {
     }
 }
 
+static void init_handle_resources(xrs_handle_t h);
+
 int xrs_create(xrs_handle_t* handle, int device) {
     return guarded([&] {
         XRS_REQUIRE(handle != nullptr, "null handle pointer");
@@ -211,15 +222,58 @@ int xrs_create(xrs_handle_t* handle, int device) {
         h->device = device;
         XRS_HIP(hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking));
         h->stream = h->own_stream;
+        // side streams 1 and 2 carry the asynchronous inner product at the lowest queue priority, so the
+        // work enqueued beside it (the round on the main stream) is dispatched first and the product
+        // fills the gaps (bench step 1.19 -> 1.16 ms). XRS_ASYNC_PRIORITY=normal|high for experiments.
+        int prio_least = 0, prio_greatest = 0;
+        (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
+        const char* ap = std::getenv("XRS_ASYNC_PRIORITY");
+        const bool ap_set = !(ap && std::strcmp(ap, "normal") == 0) && prio_least != prio_greatest;
+        const int async_prio = (ap && std::strcmp(ap, "high") == 0) ? prio_greatest : prio_least;
+        for (int i = 0; i < xrs_handle_s::kSides; ++i) {
+            if (ap_set && i >= 1)
+                XRS_HIP(hipStreamCreateWithPriority(&h->side_stream[i], hipStreamNonBlocking, async_prio));
+            else
+                XRS_HIP(hipStreamCreateWithFlags(&h->side_stream[i], hipStreamNonBlocking));
+        }
+        init_handle_resources(h);
+        *handle = h;
+    });
+}
+
+}  // extern "C"
+
+xrs_handle_t xrs::create_child_handle(xrs_handle_t parent) {
+    auto* h = new xrs_handle_s();
+    h->device = parent->device;
+    h->borrowed_streams = true;
+    h->own_stream = parent->side_stream[1];
+    h->stream = h->own_stream;
+    h->side_stream[0] = parent->side_stream[2];
+    h->side_stream[1] = parent->side_stream[1];   // (never forked to: the child forks with one side)
+    h->side_stream[2] = parent->side_stream[2];
+    try {
+        init_handle_resources(h);
+    } catch (...) {
+        delete h;
+        throw;
+    }
+    return h;
+}
+
+static void init_handle_resources(xrs_handle_t h) {
+    {
+        const int device = h->device;
         h->pool = new Pool(device);
         for (int i = 0; i < xrs_handle_s::kSides; ++i) {
-            XRS_HIP(hipStreamCreateWithFlags(&h->side_stream[i], hipStreamNonBlocking));
             h->side_pool[i] = new Pool(device);
             XRS_HIP(hipEventCreateWithFlags(&h->ev_join[i], hipEventDisableTiming));
         }
         XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
         XRS_HIP(hipEventCreateWithFlags(&h->ev_aux, hipEventDisableTiming));
         XRS_HIP(hipEventCreateWithFlags(&h->ev_host, hipEventDisableTiming));
+        XRS_HIP(hipEventCreateWithFlags(&h->ev_dot, hipEventDisableTiming));
+        XRS_HIP(hipEventCreateWithFlags(&h->ev_dot_join, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
         const size_t tbytes = size_t(1 + xrs_handle_s::kSides) * xrs_handle_s::kTicketCap * sizeof(int);
@@ -232,14 +286,16 @@ int xrs_create(xrs_handle_t* handle, int device) {
             h->side_tickets[i] = h->ticket_base + size_t(1 + i) * xrs_handle_s::kTicketCap;
         // the zeroed tickets / sync words must be in place before any (non-blocking) stream uses them
         XRS_HIP(hipDeviceSynchronize());
-        *handle = h;
-    });
+    }
 }
+
+extern "C" {
 
 int xrs_destroy(xrs_handle_t h) {
     return guarded([&] {
         if (!h) return;
         (void)hipSetDevice(h->device);
+        destroy_dot_worker(h);   // (joins the worker thread and destroys its child handle)
         (void)hipStreamSynchronize(h->stream);
         for (auto& r : h->prof) {
             (void)hipEventDestroy(r.start);
@@ -251,17 +307,19 @@ int xrs_destroy(xrs_handle_t h) {
         delete h->pool;
         for (int i = 0; i < xrs_handle_s::kSides; ++i) {
             delete h->side_pool[i];
-            if (h->side_stream[i]) (void)hipStreamDestroy(h->side_stream[i]);
+            if (h->side_stream[i] && !h->borrowed_streams) (void)hipStreamDestroy(h->side_stream[i]);
             if (h->ev_join[i]) (void)hipEventDestroy(h->ev_join[i]);
         }
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
         if (h->ev_aux) (void)hipEventDestroy(h->ev_aux);
         if (h->ev_host) (void)hipEventDestroy(h->ev_host);
+        if (h->ev_dot) (void)hipEventDestroy(h->ev_dot);
+        if (h->ev_dot_join) (void)hipEventDestroy(h->ev_dot_join);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
         (void)hipFree(h->ticket_base);
         (void)hipFree(h->sync_words);
-        if (h->own_stream) (void)hipStreamDestroy(h->own_stream);
+        if (h->own_stream && !h->borrowed_streams) (void)hipStreamDestroy(h->own_stream);
         delete h;
     });
 }
@@ -295,7 +353,9 @@ int xrs_malloc(xrs_handle_t h, void** ptr, size_t bytes) {
 int xrs_free(xrs_handle_t h, void* ptr) {
     return guarded([&] {
         XRS_REQUIRE(h, "null handle");
-        if (ptr) h->pool->release(ptr);
+        if (!ptr) return;
+        fence_readers(h);
+        h->pool->release(ptr);
     });
 }
 
@@ -345,6 +405,13 @@ int xrs_prof_end(xrs_handle_t h, size_t* launches, double* total_ms, double* flo
         XRS_REQUIRE(h, "null handle");
         h->prof_mask = 0;
         XRS_HIP(hipStreamSynchronize(h->stream));
+        // records of the asynchronous inner product's worker (its child handle), once it has finished
+        if (xrs_handle_t c = dot_child(h)) {
+            wait_dot_done(h);
+            c->prof_mask = 0;
+            h->prof.insert(h->prof.end(), c->prof.begin(), c->prof.end());
+            c->prof.clear();
+        }
         double ms = 0, f = 0, b = 0;
         for (auto& r : h->prof) {
             float t = 0;

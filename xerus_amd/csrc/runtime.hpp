@@ -79,6 +79,11 @@ struct ProfRecord {
 
 }  // namespace xrs
 
+namespace xrs {
+class DotWorker;
+void destroy_dot_worker(xrs_handle_t h);   // tt.hip
+}  // namespace xrs
+
 struct xrs_handle_s {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -107,6 +112,15 @@ struct xrs_handle_s {
     int* side_tickets[kSides] = {};
     // algorithm of the last TT round (XRS_ROUND_*)
     int last_round_path = 0;
+    // asynchronous TT inner product (xrs_tt_dot_async): enqueued by a worker thread on a child handle
+    // whose streams are side streams 1 and 2 of this one (forked at ev_dot from the main stream), so the
+    // caller's thread goes on enqueueing the next work at once; while `reader_pending`, releases of the
+    // handle's blocks first wait until the product has finished (fence_readers)
+    hipEvent_t ev_dot = nullptr, ev_dot_join = nullptr;
+    bool reader_pending = false;
+    bool dot_pending = false;
+    xrs::DotWorker* dot_worker = nullptr;
+    bool borrowed_streams = false;   // child handle: streams belong to the parent
     // profiler
     uint32_t prof_mask = 0;
     std::vector<xrs::ProfRecord> prof;
@@ -157,6 +171,19 @@ void check_launch(const char* what);
 // check values). XRS_SYNC_SPIN=1 polls an event instead of hipStreamSynchronize (measured: no difference,
 // 1.3361 vs 1.3305 ms/step).
 void host_wait(xrs_handle_t h);
+
+// Order the current stream after an in-flight asynchronous reader of the handle's blocks (the async
+// TT inner product); no-op when none is pending. Called before a block is released and before a TT
+// is mutated in place.
+void fence_readers(xrs_handle_t h);
+// blocks until the handle's asynchronous inner product (if any) has finished on the device (tt.hip)
+void wait_dot_done(xrs_handle_t h);
+// the worker's child handle (null before the first asynchronous inner product; tt.hip)
+xrs_handle_t dot_child(xrs_handle_t h);
+
+// Child handle for a worker thread: own pools, scratch, events and split-K tickets; main stream = the
+// parent's side stream 1, side stream 0 = the parent's side stream 2 (borrowed, not destroyed).
+xrs_handle_t create_child_handle(xrs_handle_t parent);
 
 // Fork/join of independent work onto the handle's side stream. While `side()` is active every launch
 // and DevBuf of the handle goes to the side stream / side pool (stream-ordered reuse stays valid);

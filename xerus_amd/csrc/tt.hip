@@ -17,7 +17,11 @@
 // max_rank >= r, no singular value can be cut, so the SVD is skipped and B = L Q is used directly:
 // same represented tensor, same ranks, different (equally valid) orthogonal gauge.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cmath>
@@ -226,10 +230,45 @@ void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool d
     if (do_reduce) t.reduce(H[k], a * a);
 }
 
-// Both chains (G: left Grams, only with `left`; H: right Grams; `store` owns the memory). Unsharded they
-// run concurrently (left on a side stream, right on the main stream) with their launches interleaved
-// step by step, so that neither stream waits for the host to finish enqueueing the other chain. Sharded,
-// step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s} sit side by side in one buffer.
+// Step s of both chains as paired launches (gemm_pair): the two T products in one grid, then the two
+// Grams in one grid; with dry = true only reports whether both pairs would be taken. Boundary cores
+// (k = 0 left, k = d-1 right) have their own single products.
+bool paired_gram_step(TT& t, std::vector<double*>& G, std::vector<double*>& H, double* TL, double* TR, size_t kl, size_t kr,
+                      bool dry) {
+    const size_t last = t.d - 1;
+    if (kl == 0 || kr == last) {
+        if (dry) return false;
+        left_gram_step(t, G, TL, kl);
+        right_gram_step(t, H, TR, kr);
+        return false;
+    }
+    const size_t a = t.r[kl], b = t.r[kl + 1], cl = t.cols_right(kl);
+    const size_t a2 = t.r[kr], b2 = t.r[kr + 1], cr = t.cols_right(kr);
+    const GemmSpec l1{G[kl], t.core[kl], TL, a, cl, a, a, cl, false, false};               // G_k M_k
+    const GemmSpec r1{t.core[kr], H[kr + 1], TR, a2 * t.n[kr], b2, b2, b2, b2, false, false};  // M_k H_{k+1}
+    const GemmSpec l2{t.core[kl], TL, G[kl + 1], b, b, a * t.n[kl], b, b, true, false};      // M^T (G M)
+    const GemmSpec r2{t.core[kr], TR, H[kr], a2, a2, cr, cr, cr, false, true};               // M (M H)^T
+    if (dry) return gemm_pair(t.h, l1, r1, false, true) && gemm_pair(t.h, l2, r2, true, true);
+    bool paired = true;
+    if (!gemm_pair(t.h, l1, r1)) {
+        gemm(t.h, l1);
+        gemm(t.h, r1);
+        paired = false;
+    }
+    if (!gemm_pair(t.h, l2, r2, true)) {
+        gemm_sym(t.h, l2.C, l2.N, 1.0, l2.A, l2.lda, l2.ta, l2.K, l2.B, l2.ldb, l2.tb);
+        gemm_sym(t.h, r2.C, r2.N, 1.0, r2.A, r2.lda, r2.ta, r2.K, r2.B, r2.ldb, r2.tb);
+        paired = false;
+    }
+    return paired;
+}
+
+// Both chains (G: left Grams, only with `left`; H: right Grams; `store` owns the memory). Unsharded,
+// when every step pairs (paired_gram_step), they run on ONE stream as paired launches -- each grid holds
+// both chains' products, so a launch fills the chip instead of two kernels sharing it from two streams;
+// otherwise concurrently (left on a side stream, right on the main stream) with their launches
+// interleaved step by step. Sharded, step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s}
+// sit side by side in one buffer.
 void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
@@ -262,6 +301,14 @@ void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::v
     }
     if (!left) {
         for (size_t k = d - 1; k >= 1; --k) right_gram_step(t, H, TR.d(), k);
+        return;
+    }
+    // one stream with paired launches when most steps pair (the unpaired ones -- boundary cores, odd
+    // ranks -- then run their two chains back to back), else two streams
+    size_t npair = 0;
+    for (size_t s = 0; s + 1 < d; ++s) npair += paired_gram_step(t, G, H, TL.d(), TR.d(), s, d - 1 - s, true) ? 1 : 0;
+    if (2 * npair >= d - 1 && npair >= 2) {
+        for (size_t s = 0; s + 1 < d; ++s) paired_gram_step(t, G, H, TL.d(), TR.d(), s, d - 1 - s, false);
         return;
     }
     StreamFork fork(h);
@@ -343,7 +390,7 @@ void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
         for (size_t j = i; j < jobs.size(); ++j) {
             const GemmJob& o = jobs[j];
             if (done[j] || o.M != g.M || o.N != g.N || o.K != g.K || o.lda != g.lda || o.ldb != g.ldb || o.ta != g.ta ||
-                o.tb != g.tb || o.sym != g.sym || o.alpha != g.alpha)
+                o.tb != g.tb || o.sym != g.sym || o.alpha != g.alpha || o.tri != g.tri)
                 continue;
             done[j] = true;
             A.push_back(o.A);
@@ -351,9 +398,9 @@ void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs) {
             C.push_back(o.C);
         }
         if (C.size() == 1 && g.sym) gemm_sym(h, C[0], g.N, g.alpha, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
-        else if (C.size() == 1) gemm(h, C[0], g.M, g.N, g.alpha, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb);
+        else if (C.size() == 1) gemm(h, C[0], g.M, g.N, g.alpha, A[0], g.lda, g.ta, g.K, B[0], g.ldb, g.tb, g.tri);
         else gemm_batched(h, int(C.size()), C.data(), g.M, g.N, g.alpha, A.data(), g.lda, g.ta, g.K, B.data(), g.ldb,
-                          g.tb, g.sym);
+                          g.tb, g.sym, g.tri);
     }
 }
 
@@ -667,14 +714,19 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
         }
         trinv_batched(h, part, c);
     }
+    // L_k and Z_k of the register-resident kernels (r <= 256) hold exact zeros above the diagonal: their
+    // zero K-blocks are skipped (5/8 of the work at r = 256)
+    static const bool no_tri = std::getenv("XRS_NO_TRI") != nullptr;
     std::vector<GemmJob> right, left;
     for (size_t k = 0; k + 1 < d; ++k) {   // right factors: M_k (I (x) L_{k+1}), (r_k n_k) x r_{k+1} x r_{k+1}
         const size_t b = t.r[k + 1];
         right.push_back({t.rows_left(k), b, b, b, b, false, false, t.core[k], Lf[k + 1].d(), k == 0 ? out.C[k] : W[k].d()});
+        right.back().tri = (b <= 256 && !no_tri) ? kTriB : 0;
     }
     for (size_t k = 1; k < d; ++k) {       // left factors: Z_k (r_k x r_k) times the r_k x (n_k r_{k+1}) unfolding
         const size_t a = t.r[k], cols = t.cols_right(k);
         left.push_back({a, cols, a, a, cols, false, false, Z[k].d(), k + 1 < d ? W[k].d() : t.core[k], out.C[k]});
+        left.back().tri = (a <= 256 && !no_tri) ? kTriA : 0;
     }
     gemm_grouped(h, right);
     gemm_grouped(h, left);
@@ -870,45 +922,88 @@ double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx
         XRS_HIP(hipMemcpyAsync(P0.d(), &ones[0], 8, hipMemcpyHostToDevice, h->stream));
         XRS_HIP(hipMemcpyAsync(P0.d() + emax, &ones[1], 8, hipMemcpyHostToDevice, h->stream));
     }
+    // per step: the left end's products (T = E^T X_k, E' = T^T Y_k) and the right end's (T = X_k F,
+    // F' = T Y_k^T); the first product of an end is skipped at a unit boundary (T = X_k)
+    struct EndStep {
+        bool on = false, first = false;
+        GemmSpec g1{}, g2{};
+    };
+    const size_t steps = std::max(m, d - m);
+    auto plan = [&](size_t s, double* E, double* F, double* nb, EndStep& L, EndStep& R, size_t& ne) {
+        L = EndStep{};
+        R = EndStep{};
+        ne = 0;
+        if (s < m) {
+            const size_t k = s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+            L.on = true;
+            L.first = !(s == 0 && unit_l);
+            const double* T = L.first ? TL.d() : X[k];
+            L.g1 = GemmSpec{E, X[k], TL.d(), b, nk * a2, a, b, nk * a2, true, false};          // E^T X_k: b x (nk a2)
+            L.g2 = GemmSpec{T, Y[k], nb, a2, b2, b * nk, a2, b2, true, false};                 // ((b nk) x a2)^T Y_k
+            ne = a2 * b2;
+        }
+        if (s < d - m) {
+            const size_t k = d - 1 - s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
+            R.on = true;
+            R.first = !(s == 0 && unit_r);
+            const double* T = R.first ? TR.d() : X[k];
+            R.g1 = GemmSpec{X[k], F, TR.d(), a * nk, b2, a2, a2, b2, false, false};            // X_k F: (a nk) x b2
+            R.g2 = GemmSpec{T, Y[k], nb + (shard ? ne : emax), a, b, nk * b2, nk * b2, nk * b2, false, true};   // T Y_k^T
+        }
+    };
+    // both ends on ONE stream as paired launches (gemm_pair) when most steps pair; else the left end on a
+    // side stream beside the right end on the main stream (and always so when sharded)
+    size_t npair = 0;
+    if (!shard) {
+        double *E = P0.d(), *F = P0.d() + emax, *nb = P1.d(), *cb = P0.d();
+        for (size_t s = 0; s < steps; ++s) {
+            EndStep L, R;
+            size_t ne;
+            plan(s, E, F, nb, L, R, ne);
+            if (L.on && R.on && L.first && R.first && gemm_pair(h, L.g1, R.g1, false, true) &&
+                gemm_pair(h, L.g2, R.g2, false, true))
+                ++npair;
+            if (L.on) E = L.g2.C;
+            if (R.on) F = R.g2.C;
+            std::swap(cb, nb);
+        }
+    }
+    const bool paired = !shard && 2 * npair >= steps && npair >= 2;
     double *E = P0.d(), *F = P0.d() + emax;
     double* nextbuf = P1.d();
     double* curbuf = P0.d();
     {
         StreamFork fork(h);
-        const size_t steps = std::max(m, d - m);
         for (size_t s = 0; s < steps; ++s) {   // launches interleaved step by step (see gram_chains)
-            double* En = E;
-            double* Fn = F;
-            size_t ne = 0, nf = 0;
-            if (s < m) {
-                if (!shard) fork.side();
-                const size_t k = s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
-                En = nextbuf;
-                ne = a2 * b2;
-                const double* T = X[k];
-                if (!(s == 0 && unit_l)) {
-                    gemm(h, TL.d(), b, nk * a2, 1.0, E, b, true, a, X[k], nk * a2, false);    // E^T X_k: b x (nk a2)
-                    T = TL.d();
+            EndStep L, R;
+            size_t ne;
+            plan(s, E, F, nextbuf, L, R, ne);
+            if (paired && L.on && R.on && L.first == R.first) {
+                if (L.first && !gemm_pair(h, L.g1, R.g1)) {
+                    gemm(h, L.g1);
+                    gemm(h, R.g1);
                 }
-                gemm(h, En, a2, b2, 1.0, T, a2, true, b * nk, Y[k], b2, false);            // ((b nk) x a2)^T Y_k
-            }
-            if (s < d - m) {
-                if (!shard) fork.main();
-                const size_t k = d - 1 - s, a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
-                Fn = nextbuf + (shard ? ne : emax);
-                nf = a * b;
-                const double* T = X[k];
-                if (!(s == 0 && unit_r)) {
-                    gemm(h, TR.d(), a * nk, b2, 1.0, X[k], a2, false, a2, F, b2, false);       // X_k F: (a nk) x b2
-                    T = TR.d();
+                if (!gemm_pair(h, L.g2, R.g2)) {
+                    gemm(h, L.g2);
+                    gemm(h, R.g2);
                 }
-                gemm(h, Fn, a, b, 1.0, T, nk * b2, false, nk * b2, Y[k], nk * b2, true);       // T Y_k^T: a x b
+            } else {
+                if (L.on) {
+                    if (!shard && !paired) fork.side();
+                    if (L.first) gemm(h, L.g1);
+                    gemm(h, L.g2);
+                }
+                if (R.on) {
+                    if (!shard && !paired) fork.main();
+                    if (R.first) gemm(h, R.g1);
+                    gemm(h, R.g2);
+                }
             }
             // one all-reduce for both ends. The left end is idle only in the last step of an odd order
             // (d - m = m + 1): E then stays in the other buffer, untouched by this step's F.
-            if (shard) shard->reduce(nextbuf, ne + nf);
-            E = En;
-            F = Fn;
+            if (shard) shard->reduce(nextbuf, ne + (R.on ? R.g2.M * R.g2.N : 0));
+            if (L.on) E = L.g2.C;
+            if (R.on) F = R.g2.C;
             std::swap(curbuf, nextbuf);
         }
         fork.join();
@@ -944,6 +1039,126 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
     return hs[0];
 }
 
+}  // namespace ttd
+
+// Asynchronous <x, y> (xrs_tt_dot_async). The caller's thread only forks (records ev_dot on the main
+// stream; the child's two streams -- side streams 1 and 2 -- wait for it) and posts the TT descriptors to
+// a persistent worker thread, which enqueues the ordinary two-ended zipper on the child handle and
+// synchronises it. The caller meanwhile enqueues its next work (x.round) on the main stream, so both
+// run on the device together and the ~25 launches of the product cost the caller no host time.
+// Releases of the parent's blocks wait for the worker to finish (fence_readers): the round's
+// replacement of x's cores never recycles a block the product still reads.
+class DotWorker {
+   public:
+    explicit DotWorker(xrs_handle_t parent) : child_(create_child_handle(parent)), th_([this] { run(); }) {}
+    ~DotWorker() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            quit_ = true;
+            state_.store(kPosted, std::memory_order_release);
+        }
+        cv_.notify_all();
+        th_.join();
+        (void)xrs_destroy(child_);
+    }
+    xrs_handle_t child() const { return child_; }
+    void post(size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+              const double* const* Y) {
+        d_ = d;
+        n_.assign(n, n + d);
+        rx_.assign(rx, rx + d + 1);
+        ry_.assign(ry, ry + d + 1);
+        X_.assign(X, X + d);
+        Y_.assign(Y, Y + d);
+        err_code_ = 0;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            state_.store(kPosted, std::memory_order_release);
+        }
+        cv_.notify_all();
+    }
+    // blocks until the posted product has finished (device included)
+    void wait_done() {
+        for (int i = 0; i < (1 << 16) && state_.load(std::memory_order_acquire) != kDone; ++i) __builtin_ia32_pause();
+        if (state_.load(std::memory_order_acquire) != kDone) {
+            std::unique_lock<std::mutex> g(m_);
+            cv_.wait(g, [&] { return state_.load(std::memory_order_acquire) == kDone; });
+        }
+    }
+    double take() {
+        wait_done();
+        state_.store(kIdle, std::memory_order_release);
+        if (err_code_ != 0) throw Error{err_code_, err_msg_};
+        return value_;
+    }
+
+   private:
+    static constexpr int kIdle = 0, kPosted = 1, kDone = 2;
+    void run() {
+        (void)hipSetDevice(child_->device);
+        for (;;) {
+            // spin briefly (the next product usually follows within a step), then sleep
+            for (int i = 0; i < (1 << 18) && state_.load(std::memory_order_acquire) != kPosted; ++i) __builtin_ia32_pause();
+            if (state_.load(std::memory_order_acquire) != kPosted) {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return state_.load(std::memory_order_acquire) == kPosted; });
+            }
+            if (quit_) return;
+            try {
+                value_ = ttd::dot(child_, d_, n_.data(), rx_.data(), X_.data(), ry_.data(), Y_.data());
+            } catch (const Error& e) {
+                err_code_ = e.code;
+                err_msg_ = e.msg;
+            } catch (const std::exception& e) {
+                err_code_ = XRS_EINVAL;
+                err_msg_ = e.what();
+            }
+            {
+                std::lock_guard<std::mutex> g(m_);
+                state_.store(kDone, std::memory_order_release);
+            }
+            cv_.notify_all();
+        }
+    }
+    xrs_handle_t child_;
+    size_t d_ = 0;
+    std::vector<size_t> n_, rx_, ry_;
+    std::vector<const double*> X_, Y_;
+    double value_ = 0.0;
+    int err_code_ = 0;
+    std::string err_msg_;
+    bool quit_ = false;
+    std::atomic<int> state_{kIdle};
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::thread th_;   // (last: started after every other member is constructed)
+};
+
+void dot_async(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+               const double* const* Y) {
+    XRS_REQUIRE(!h->dot_pending, "an asynchronous inner product is already in flight on this handle");
+    if (h->dot_worker == nullptr) h->dot_worker = new DotWorker(h);
+    xrs_handle_t c = h->dot_worker->child();
+    c->prof_mask = h->prof_mask;   // (the parent's profiler collects the child's records at prof_end)
+    XRS_HIP(hipEventRecord(h->ev_dot, h->stream));
+    XRS_HIP(hipStreamWaitEvent(c->stream, h->ev_dot, 0));
+    XRS_HIP(hipStreamWaitEvent(c->side_stream[0], h->ev_dot, 0));
+    h->dot_worker->post(d, n, rx, X, ry, Y);
+    h->dot_pending = true;
+    h->reader_pending = true;
+}
+
+double dot_wait(xrs_handle_t h) {
+    XRS_REQUIRE(h->dot_pending, "no asynchronous inner product in flight on this handle");
+    h->dot_pending = false;
+    h->reader_pending = false;
+    return h->dot_worker->take();
+}
+
+xrs_handle_t dot_child(xrs_handle_t h) { return h->dot_worker ? h->dot_worker->child() : nullptr; }
+
+namespace ttd {
+
 void check_tt(size_t d, const size_t* n, const size_t* r, double* const* cores) {
     XRS_REQUIRE(d >= 1, "TT must have at least one component");
     XRS_REQUIRE(n && r && cores, "null TT description");
@@ -957,6 +1172,23 @@ void check_tt(size_t d, const size_t* n, const size_t* r, double* const* cores) 
 }  // namespace ttd
 
 using namespace ttd;
+
+void wait_dot_done(xrs_handle_t h) {
+    if (h->dot_pending && h->dot_worker != nullptr) h->dot_worker->wait_done();
+}
+
+void destroy_dot_worker(xrs_handle_t h) {
+    if (h->dot_worker == nullptr) return;
+    if (h->dot_pending) {
+        try {
+            (void)h->dot_worker->take();
+        } catch (...) {
+        }
+        h->dot_pending = false;
+    }
+    delete h->dot_worker;
+    h->dot_worker = nullptr;
+}
 
 namespace tt {
 void move_core(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
@@ -1052,6 +1284,24 @@ int xrs_tt_dot(xrs_handle_t h, double* result, size_t d, const size_t* n, const 
         check_tt(d, n, rx, const_cast<double* const*>(X));
         check_tt(d, n, ry, const_cast<double* const*>(Y));
         *result = dot(h, d, n, rx, X, ry, Y);
+    });
+}
+
+int xrs_tt_dot_async(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X,
+                     const size_t* ry, const double* const* Y) {
+    return guarded([&] {
+        XRS_REQUIRE(h, "null handle");
+        check_tt(d, n, rx, const_cast<double* const*>(X));
+        check_tt(d, n, ry, const_cast<double* const*>(Y));
+        XRS_REQUIRE(d >= 2, "the asynchronous inner product needs at least two components");
+        dot_async(h, d, n, rx, X, ry, Y);
+    });
+}
+
+int xrs_tt_dot_wait(xrs_handle_t h, double* result) {
+    return guarded([&] {
+        XRS_REQUIRE(h && result, "null argument");
+        *result = dot_wait(h);
     });
 }
 

@@ -20,7 +20,11 @@ struct TT {
     size_t size(size_t k) const { return r[k] * n[k] * r[k + 1]; }
 
     double* alloc(size_t elems) { return static_cast<double*>(h->pool->alloc(std::max<size_t>(elems, 1) * 8)); }
-    void release(double* p) { if (p) h->pool->release(p); }
+    void release(double* p) {
+        if (!p) return;
+        fence_readers(h);   // an in-flight async inner product may still read the block
+        h->pool->release(p);
+    }
     void replace(size_t k, double* p) { release(core[k]); core[k] = p; }
 
     // Mode-sharded TT (xrs_tt_*_sharded): n[] are this rank's slice counts and every sum over the
@@ -69,6 +73,7 @@ struct GemmJob {
     double* C;
     bool sym = false;   // result known symmetric (M == N): lower tiles only, mirrored
     double alpha = 1.0;
+    int tri = 0;        // triangular operands (kTriA / kTriB, gemm): zero K-blocks skipped
 };
 void gemm_grouped(xrs_handle_t h, const std::vector<GemmJob>& jobs);
 
