@@ -608,6 +608,7 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     std::vector<DevBuf> gram_store, Lf(d), Cs;
     XRS_MARK("pass");
     gram_chains(t, G, H, gram_store, certify);
+    open_dot_gate(h);   // a gated async <x,y> runs beside the factorisations and transforms below
     XRS_MARK("chains");
     // edges with r <= 256: one batched register-resident launch; larger (<= 512): factor_big (2 x 2
     // blocks of the same kernels), which also delivers Z = L^{-1}
@@ -1056,14 +1057,19 @@ class DotWorker {
             std::lock_guard<std::mutex> g(m_);
             quit_ = true;
             state_.store(kPosted, std::memory_order_release);
+            gate_.store(1, std::memory_order_release);
         }
         cv_.notify_all();
         th_.join();
         (void)xrs_destroy(child_);
     }
     xrs_handle_t child() const { return child_; }
+    // gated: the worker enqueues only once open_gate() has been called (with gate_ev: the child's streams
+    // first wait for that event)
     void post(size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
-              const double* const* Y) {
+              const double* const* Y, bool gated) {
+        gate_ev_ = nullptr;
+        gate_.store(gated ? 0 : 1, std::memory_order_release);
         d_ = d;
         n_.assign(n, n + d);
         rx_.assign(rx, rx + d + 1);
@@ -1077,8 +1083,19 @@ class DotWorker {
         }
         cv_.notify_all();
     }
+    void open_gate(hipEvent_t ev) {
+        if (gate_.load(std::memory_order_acquire) != 0) return;
+        gate_ev_ = ev;
+        {
+            std::lock_guard<std::mutex> g(m_);
+            gate_.store(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+    }
+    bool gate_closed() const { return gate_.load(std::memory_order_acquire) == 0; }
     // blocks until the posted product has finished (device included)
     void wait_done() {
+        open_gate(nullptr);
         for (int i = 0; i < (1 << 16) && state_.load(std::memory_order_acquire) != kDone; ++i) __builtin_ia32_pause();
         if (state_.load(std::memory_order_acquire) != kDone) {
             std::unique_lock<std::mutex> g(m_);
@@ -1104,7 +1121,17 @@ class DotWorker {
                 cv_.wait(g, [&] { return state_.load(std::memory_order_acquire) == kPosted; });
             }
             if (quit_) return;
+            for (int i = 0; i < (1 << 18) && gate_.load(std::memory_order_acquire) == 0; ++i) __builtin_ia32_pause();
+            if (gate_.load(std::memory_order_acquire) == 0) {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gate_.load(std::memory_order_acquire) != 0 || quit_; });
+            }
+            if (quit_) return;
             try {
+                if (gate_ev_ != nullptr) {
+                    XRS_HIP(hipStreamWaitEvent(child_->stream, gate_ev_, 0));
+                    XRS_HIP(hipStreamWaitEvent(child_->side_stream[0], gate_ev_, 0));
+                }
                 value_ = ttd::dot(child_, d_, n_.data(), rx_.data(), X_.data(), ry_.data(), Y_.data());
             } catch (const Error& e) {
                 err_code_ = e.code;
@@ -1129,6 +1156,8 @@ class DotWorker {
     std::string err_msg_;
     bool quit_ = false;
     std::atomic<int> state_{kIdle};
+    std::atomic<int> gate_{1};
+    hipEvent_t gate_ev_ = nullptr;
     std::mutex m_;
     std::condition_variable cv_;
     std::thread th_;   // (last: started after every other member is constructed)
@@ -1143,9 +1172,23 @@ void dot_async(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
     XRS_HIP(hipEventRecord(h->ev_dot, h->stream));
     XRS_HIP(hipStreamWaitEvent(c->stream, h->ev_dot, 0));
     XRS_HIP(hipStreamWaitEvent(c->side_stream[0], h->ev_dot, 0));
-    h->dot_worker->post(d, n, rx, X, ry, Y);
+    // Gate (default; XRS_DOT_GATE=0: start at once): the product starts behind the Gram chains of the next
+    // round on this handle (open_dot_gate, called by chain_pass), so that it fills the round's
+    // factorisation phase -- one batched Cholesky launch on a few CUs -- instead of halving the chains'
+    // share of the chip. Anything that waits for the product opens the gate first.
+    static const bool gate = [] {
+        const char* e = std::getenv("XRS_DOT_GATE");
+        return !(e && e[0] == '0');
+    }();
+    h->dot_worker->post(d, n, rx, X, ry, Y, gate);
     h->dot_pending = true;
     h->reader_pending = true;
+}
+
+void open_dot_gate(xrs_handle_t h) {
+    if (!h->dot_pending || h->dot_worker == nullptr || !h->dot_worker->gate_closed()) return;
+    XRS_HIP(hipEventRecord(h->ev_dot_join, h->stream));
+    h->dot_worker->open_gate(h->ev_dot_join);
 }
 
 double dot_wait(xrs_handle_t h) {

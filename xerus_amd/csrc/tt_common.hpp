@@ -6,6 +6,9 @@
 #include "smallla.hpp"
 
 namespace xrs {
+// start a gated asynchronous inner product of the handle behind its current stream point (tt.hip)
+void open_dot_gate(xrs_handle_t h);
+
 namespace ttd {
 
 struct TT {

@@ -190,6 +190,7 @@ void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<
     double* T = sw.buf(tmax);
     for (size_t k = 1; k < d; ++k) G[k] = sw.buf(t.r[k] * t.r[k]);
     for (size_t k = 0; k + 1 < d; ++k) left_gram_step(t, G, T, k, true);   // (sharded: + one all-reduce per step)
+    open_dot_gate(h);   // a gated async <x,y> runs beside the factorisations below
     std::vector<double*> Lf(d, nullptr), Zf(d, nullptr);
     std::vector<CholJob> jobs;
     for (size_t k = 1; k < d; ++k) {
