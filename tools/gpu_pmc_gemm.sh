@@ -1,9 +1,10 @@
 # PMC passes (one rocprofv3 --pmc run each) over single TT-shape GEMMs: XRS_GEMM_GLDS variant x shape
 set -o pipefail
+mkdir -p gpurun_out/pmcg
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES"
 P2="SQ_INSTS_LDS SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE"
-for cfg in "6,256:NN wide" "-1,256:Gram M^T" "0,256:NN wide"; do
+for cfg in ${PMC_CFGS:-"6,256:NN wide" "-1,256:Gram M^T" "-1,256:right chain"}; do
   v=${cfg%%:*}; shape=${cfg#*:}; tag=$(echo "$v$shape" | tr -c 'a-zA-Z0-9' '_')
   for p in 1 2; do
     eval C=\$P$p

@@ -411,16 +411,16 @@ __device__ __forceinline__ void gemm_body(const PTR& ptrs, size_t lda, size_t ld
 // Fragment reads (16 rows x k, k+1 per 32-lane half) then hit 32 distinct 8-B bank pairs in both images.
 constexpr int kGldsBK = 32;
 
-template <int R, bool KMAJ>
+template <int R, bool KMAJ, int BK = kGldsBK>
 struct GldsImg {
     // k-major rows of R % 32 == 16 doubles alternate bank halves by themselves (640-B rows: k*160 words mod 64 =
     // 0, 32, ...); rows of whole 256-B bank rows take the XOR
     static_assert(!KMAJ || R % 16 == 0, "k-major image rows must be whole MFMA tiles");
     static constexpr int KSWZ = (R % 32 == 0) ? 8 : 0;
-    static constexpr int DOUBLES = R * kGldsBK;
+    static constexpr int DOUBLES = R * BK;
     static constexpr int INSTR = DOUBLES * 8 / 1024;   // 1-KB wave instructions per stage
     __device__ static int at(int r, int k) {   // LDS offset (doubles) of element (r, k)
-        if constexpr (!KMAJ) return r * kGldsBK + ((((k >> 1) ^ (r & 15))) << 1) + (k & 1);
+        if constexpr (!KMAJ) return r * BK + ((((k >> 1) ^ (r & 15))) << 1) + (k & 1);
         else return k * R + ((((r >> 1) ^ ((k & 1) * KSWZ))) << 1) + (r & 1);
     }
     // Per-lane fragment offsets of the NF 16-row MFMA fragments at rows w0 + 16 i (w0 % 16 == 0) for
@@ -436,7 +436,7 @@ struct GldsImg {
         __device__ Frag(int w0, int kg, int lane) {
             const int lr = lane & 15, lk = lane >> 4;
             if constexpr (!KMAJ) {
-                base[0] = (w0 + lr) * kGldsBK + (lk & 1);
+                base[0] = (w0 + lr) * BK + (lk & 1);
                 z = (2 * kg) ^ (lk >> 1) ^ lr;
             } else {
                 const int swz = (lk & 1) * (KSWZ / 8);
@@ -445,14 +445,15 @@ struct GldsImg {
             }
         }
         __device__ int off(int q, int i) const {
-            if constexpr (!KMAJ) return base[0] + i * 16 * kGldsBK + (((2 * q * WGK) ^ z) << 1);
+            if constexpr (!KMAJ) return base[0] + i * 16 * BK + (((2 * q * WGK) ^ z) << 1);
             else return base[i] + 4 * q * WGK * R;
         }
     };
     __device__ static void src(int q, int& r, int& k) {   // element (r, k) that starts LDS chunk q
         if constexpr (!KMAJ) {
-            r = q >> 4;
-            k = ((q & 15) ^ (r & 15)) << 1;
+            constexpr int CPR = BK / 2;   // 16-B chunks per row
+            r = q / CPR;
+            k = ((q % CPR) ^ (r & 15)) << 1;
         } else {
             constexpr int CR = R / 2;
             k = q / CR;
@@ -464,26 +465,30 @@ struct GldsImg {
 template <int BM, int BN, int WGM, int WGN, int WGK>
 constexpr int glds_min_waves() { return (WGM * WGN * WGK * 64 >= 512) ? 2 : 1; }
 
-// LDS of the glds pipeline: S = 3 stages of the A and B images
-template <int BM, int BN>
-constexpr int glds_lds_doubles() { return 3 * (BM + BN) * kGldsBK; }
+// LDS of the glds pipeline: S stages of the A and B images -- 3 stages of 32-deep K-steps, or 2 stages
+// of 64-deep steps (half the barriers per K; the DMA of step t+1 is issued at the start of step t, the
+// same 64-deep lead as 3 x 32)
+template <int BK>
+constexpr int glds_stages() { return BK == 64 ? 2 : 3; }
+template <int BM, int BN, int BK = kGldsBK>
+constexpr int glds_lds_doubles() { return glds_stages<BK>() * (BM + BN) * BK; }
 
 // One output tile of the glds pipeline for entry blockIdx.y of `ptrs` (tile blockIdx.x, K-slice
 // blockIdx.z); `lds` holds glds_lds_doubles<BM, BN>() doubles. Shared by k_gemm_glds (one shape per
 // launch) and k_gemm_glds2 (two entries of different shapes / transposes in one launch).
-template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR>
+template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK>
 __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& ptrs, size_t lda, size_t ldb, int M, int N,
                                           int K, int kps, double alpha, double* __restrict__ slab, int tiles_m,
                                           int xcd_group, int* __restrict__ tickets, int sym, int tri) {
 #ifdef XRS_GEMM_TRACE
     const unsigned long long xrs_c0 = __builtin_amdgcn_s_memtime();
 #endif
-    constexpr int BK = kGldsBK, S = 3;
+    constexpr int S = glds_stages<BK>();
     constexpr int NW = WGM * WGN * WGK;
-    using IA = GldsImg<BM, TA>;   // A stored [m][k] (RK) or, transposed, [k][m] (KR)
-    using IB = GldsImg<BN, !TB>;  // B stored [k][n] (KR) or, transposed, [n][k] (RK)
+    using IA = GldsImg<BM, TA, BK>;   // A stored [m][k] (RK) or, transposed, [k][m] (KR)
+    using IB = GldsImg<BN, !TB, BK>;  // B stored [k][n] (KR) or, transposed, [n][k] (RK)
     constexpr int STAGE = IA::DOUBLES + IB::DOUBLES;
-    static_assert(S * STAGE == glds_lds_doubles<BM, BN>(), "LDS layout");
+    static_assert(S * STAGE == glds_lds_doubles<BM, BN, BK>(), "LDS layout");
     constexpr int INSTR = IA::INSTR + IB::INSTR;
     // wave w issues DMA instructions j = w, w + NW, ...: PER_WAVE of them, or one fewer for w >= INSTR % NW
     constexpr int PER_WAVE = (INSTR + NW - 1) / NW;
@@ -614,14 +619,14 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
     gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, lds, ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
 }
 
-template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR>
+template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64, (glds_min_waves<BM, BN, WGM, WGN, WGK>()))
 k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
             double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym, int tri) {
     XRS_TRACE_BEGIN
-    __shared__ double lds[glds_lds_doubles<BM, BN>()];   // the one LDS array (trap 4a: no second __shared__ object)
-    glds_body<BM, BN, WGM, WGN, WGK, TA, TB, PTR>(lds, ptrs, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xcd_group,
-                                                  tickets, sym, tri);
+    __shared__ double lds[glds_lds_doubles<BM, BN, BK>()];   // the one LDS array (trap 4a: no second __shared__ object)
+    glds_body<BM, BN, WGM, WGN, WGK, TA, TB, PTR, BK>(lds, ptrs, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xcd_group,
+                                                      tickets, sym, tri);
     XRS_TRACE_END
 }
 
@@ -710,7 +715,7 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
     check_launch("k_gemm_f64");
 }
 
-template <int BM, int BN, int WGM, int WGN, int WGK, class PTR>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK = kGldsBK, class PTR>
 static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, bool ta, size_t ldb, bool tb, int M, int N,
                         int K, int splits, int kps, double alpha, double* slab, int* tickets, int sym, int tri) {
     const int tiles_m = M / BM, tiles_n = N / BN;
@@ -724,17 +729,17 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
     double kdepth = double(K);
     if (tri & 1) {
         double s = 0;
-        for (int m0 = 0; m0 < M; m0 += BM) s += std::min(K, (m0 + BM + kGldsBK - 1) / kGldsBK * kGldsBK);
+        for (int m0 = 0; m0 < M; m0 += BM) s += std::min(K, (m0 + BM + BK - 1) / BK * BK);
         kdepth = s / tiles_m;
     } else if (tri & 2) {
         double s = 0;
-        for (int n0 = 0; n0 < N; n0 += BN) s += K - (n0 / kGldsBK) * kGldsBK;
+        for (int n0 = 0; n0 < N; n0 += BN) s += K - (n0 / BK) * BK;
         kdepth = s / tiles_n;
     }
     KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * kdepth,
                       count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GLDS_LAUNCH(TA_, TB_)                                                                              \
-    hipLaunchKernelGGL((k_gemm_glds<BM, BN, WGM, WGN, WGK, TA_, TB_, PTR>), grid, dim3(WGM * WGN * WGK * 64), 0, \
+    hipLaunchKernelGGL((k_gemm_glds<BM, BN, WGM, WGN, WGK, TA_, TB_, PTR, BK>), grid, dim3(WGM * WGN * WGK * 64), 0, \
                        h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets, sym, tri)
     if (!ta && !tb) XRS_GLDS_LAUNCH(false, false);
     else if (!ta && tb) XRS_GLDS_LAUNCH(false, true);
@@ -779,7 +784,12 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         // 19.4; Grams 256^2 x 5120 g4 22.3-23.7, g3 23.4-25.2, g11 24.3-24.6 (old 25.5-28.0); 512x10240x512
         // and 512^2 x 10240: g4 117.8-125 (old 126-128)
         var = 0;
-        if (sym) {
+        static const int sym_var = [] {   // XRS_GLDS_SYM_VAR: tile variant of symmetric Grams (experiments)
+            const char* e = std::getenv("XRS_GLDS_SYM_VAR");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (sym && sym_var > 0 && sym_var <= 11 && fits(sym_var)) var = sym_var;
+        else if (sym) {
             if (fits(4)) var = 4;
             else if (fits(5)) var = 5;
         } else if (fits(6) && ntiles(6) >= 192) var = 6;
@@ -789,12 +799,18 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         if (var == 0) return false;
     }
     if (var < 1 || var > 11 || !fits(var)) return false;
-    // split-K: whole 32-deep steps per slice, aiming at `target` workgroups
+    // 64-deep K-steps in 2 stages for the 8-wave tiles (XRS_GLDS_BK=64: experiment)
+    static const int bk_pref = [] {
+        const char* e = std::getenv("XRS_GLDS_BK");
+        return e ? std::atoi(e) : 32;
+    }();
+    const int bk = (bk_pref == 64 && K % 64 == 0 && (var == 4 || var == 6 || var == 7)) ? 64 : kGldsBK;
+    // split-K: whole K-steps per slice, aiming at `target` workgroups
     const long tiles = ntiles(var);
-    const int ksteps = K / kGldsBK;
+    const int ksteps = K / bk;
     int splits = 1;
-    if (tiles < g_target) splits = int(std::min<long>((g_target + tiles - 1) / tiles, std::max(1, ksteps / 4)));
-    int kps = (ksteps + splits - 1) / splits * kGldsBK;
+    if (tiles < g_target) splits = int(std::min<long>((g_target + tiles - 1) / tiles, std::max(1, ksteps * bk / 128)));
+    int kps = (ksteps + splits - 1) / splits * bk;
     splits = (K + kps - 1) / kps;
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
@@ -806,9 +822,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
         case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
         case 3: XRS_GLDS(64, 64, 2, 2, 1); break;
-        case 4: XRS_GLDS(64, 64, 2, 2, 2); break;
-        case 6: XRS_GLDS(64, 80, 4, 1, 2); break;
-        case 7: XRS_GLDS(80, 64, 1, 4, 2); break;
+        case 4: if (bk == 64) XRS_GLDS(64, 64, 2, 2, 2, 64); else XRS_GLDS(64, 64, 2, 2, 2); break;
+        case 6: if (bk == 64) XRS_GLDS(64, 80, 4, 1, 2, 64); else XRS_GLDS(64, 80, 4, 1, 2); break;
+        case 7: if (bk == 64) XRS_GLDS(80, 64, 1, 4, 2, 64); else XRS_GLDS(80, 64, 1, 4, 2); break;
         case 8: XRS_GLDS(64, 80, 2, 1, 2); break;
         case 9: XRS_GLDS(80, 64, 1, 2, 2); break;
         case 10: XRS_GLDS(64, 64, 1, 1, 4); break;
