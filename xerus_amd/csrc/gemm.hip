@@ -468,27 +468,27 @@ constexpr int glds_min_waves() { return (WGM * WGN * WGK * 64 >= 512) ? 2 : 1; }
 // LDS of the glds pipeline: S stages of the A and B images -- 3 stages of 32-deep K-steps, or 2 stages
 // of 64-deep steps (half the barriers per K; the DMA of step t+1 is issued at the start of step t, the
 // same 64-deep lead as 3 x 32)
-template <int BK>
-constexpr int glds_stages() { return BK == 64 ? 2 : 3; }
-template <int BM, int BN, int BK = kGldsBK>
-constexpr int glds_lds_doubles() { return glds_stages<BK>() * (BM + BN) * BK; }
+template <int BK, int ST = 0>
+constexpr int glds_stages() { return ST > 0 ? ST : (BK == 64 ? 2 : 3); }
+template <int BM, int BN, int BK = kGldsBK, int ST = 0>
+constexpr int glds_lds_doubles() { return glds_stages<BK, ST>() * (BM + BN) * BK; }
 
 // One output tile of the glds pipeline for entry blockIdx.y of `ptrs` (tile blockIdx.x, K-slice
 // blockIdx.z); `lds` holds glds_lds_doubles<BM, BN>() doubles. Shared by k_gemm_glds (one shape per
 // launch) and k_gemm_glds2 (two entries of different shapes / transposes in one launch).
-template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK>
+template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK, int ST = 0>
 __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& ptrs, size_t lda, size_t ldb, int M, int N,
                                           int K, int kps, double alpha, double* __restrict__ slab, int tiles_m,
                                           int xcd_group, int* __restrict__ tickets, int sym, int tri) {
 #ifdef XRS_GEMM_TRACE
     const unsigned long long xrs_c0 = __builtin_amdgcn_s_memtime();
 #endif
-    constexpr int S = glds_stages<BK>();
+    constexpr int S = glds_stages<BK, ST>();
     constexpr int NW = WGM * WGN * WGK;
     using IA = GldsImg<BM, TA, BK>;   // A stored [m][k] (RK) or, transposed, [k][m] (KR)
     using IB = GldsImg<BN, !TB, BK>;  // B stored [k][n] (KR) or, transposed, [n][k] (RK)
     constexpr int STAGE = IA::DOUBLES + IB::DOUBLES;
-    static_assert(S * STAGE == glds_lds_doubles<BM, BN, BK>(), "LDS layout");
+    static_assert(S * STAGE == glds_lds_doubles<BM, BN, BK, ST>(), "LDS layout");
     constexpr int INSTR = IA::INSTR + IB::INSTR;
     // wave w issues DMA instructions j = w, w + NW, ...: PER_WAVE of them, or one fewer for w >= INSTR % NW
     constexpr int PER_WAVE = (INSTR + NW - 1) / NW;
@@ -581,10 +581,17 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
     for (int s = 0; s < S - 1; ++s)
         if (s < nsteps) issue(s);
     for (int t = 0; t < nsteps; ++t) {
-        // retire stage t (this wave's DMAs); the next stage's stay in flight across the barrier
-        if (t + 1 >= nsteps) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else if (full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE * (S - 2)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PER_WAVE - 1) * (S - 2)) : "memory");
+        // retire stage t (this wave's DMAs); the stages issued after it (up to S - 2 of them, fewer at the
+        // end of the slice) stay in flight across the barrier
+        const int ahead = min(S - 2, nsteps - 1 - t);
+        if (ahead <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (ahead == 1) {
+            if (full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE - 1) : "memory");
+        } else {
+            if (full) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_WAVE * (S - 2)) : "memory");
+            else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PER_WAVE - 1) * (S - 2)) : "memory");
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads of stage t-1 are done
         __builtin_amdgcn_s_barrier();
         XRS_TRACE_STEP(t)
@@ -619,13 +626,13 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
     gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, lds, ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
 }
 
-template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK>
+template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK, int ST = 0>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64, (glds_min_waves<BM, BN, WGM, WGN, WGK>()))
 k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps, double alpha,
             double* __restrict__ slab, int tiles_m, int xcd_group, int* __restrict__ tickets, int sym, int tri) {
     XRS_TRACE_BEGIN
-    __shared__ double lds[glds_lds_doubles<BM, BN, BK>()];   // the one LDS array (trap 4a: no second __shared__ object)
-    glds_body<BM, BN, WGM, WGN, WGK, TA, TB, PTR, BK>(lds, ptrs, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xcd_group,
+    __shared__ double lds[glds_lds_doubles<BM, BN, BK, ST>()];   // the one LDS array (trap 4a: no second __shared__ object)
+    glds_body<BM, BN, WGM, WGN, WGK, TA, TB, PTR, BK, ST>(lds, ptrs, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xcd_group,
                                                       tickets, sym, tri);
     XRS_TRACE_END
 }
@@ -715,7 +722,7 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
     check_launch("k_gemm_f64");
 }
 
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK = kGldsBK, class PTR>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK = kGldsBK, int ST = 0, class PTR>
 static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, bool ta, size_t ldb, bool tb, int M, int N,
                         int K, int splits, int kps, double alpha, double* slab, int* tickets, int sym, int tri) {
     const int tiles_m = M / BM, tiles_n = N / BN;
@@ -739,7 +746,7 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
     KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * kdepth,
                       count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GLDS_LAUNCH(TA_, TB_)                                                                              \
-    hipLaunchKernelGGL((k_gemm_glds<BM, BN, WGM, WGN, WGK, TA_, TB_, PTR, BK>), grid, dim3(WGM * WGN * WGK * 64), 0, \
+    hipLaunchKernelGGL((k_gemm_glds<BM, BN, WGM, WGN, WGK, TA_, TB_, PTR, BK, ST>), grid, dim3(WGM * WGN * WGK * 64), 0, \
                        h->stream, P, lda, ldb, M, N, K, kps, alpha, slab, tiles_m, xg, tickets, sym, tri)
     if (!ta && !tb) XRS_GLDS_LAUNCH(false, false);
     else if (!ta && tb) XRS_GLDS_LAUNCH(false, true);
@@ -804,7 +811,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         const char* e = std::getenv("XRS_GLDS_BK");
         return e ? std::atoi(e) : 32;
     }();
+    // XRS_GLDS_BK=4: 32-deep steps in 4 stages (a 3-step DMA lead; experiment)
     const int bk = (bk_pref == 64 && K % 64 == 0 && (var == 4 || var == 6 || var == 7)) ? 64 : kGldsBK;
+    const bool st4 = bk_pref == 4 && (var == 4 || var == 6 || var == 7);
     // split-K: whole K-steps per slice, aiming at `target` workgroups
     const long tiles = ntiles(var);
     const int ksteps = K / bk;
@@ -822,9 +831,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
         case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
         case 3: XRS_GLDS(64, 64, 2, 2, 1); break;
-        case 4: if (bk == 64) XRS_GLDS(64, 64, 2, 2, 2, 64); else XRS_GLDS(64, 64, 2, 2, 2); break;
-        case 6: if (bk == 64) XRS_GLDS(64, 80, 4, 1, 2, 64); else XRS_GLDS(64, 80, 4, 1, 2); break;
-        case 7: if (bk == 64) XRS_GLDS(80, 64, 1, 4, 2, 64); else XRS_GLDS(80, 64, 1, 4, 2); break;
+        case 4: if (bk == 64) XRS_GLDS(64, 64, 2, 2, 2, 64); else if (st4) XRS_GLDS(64, 64, 2, 2, 2, 32, 4); else XRS_GLDS(64, 64, 2, 2, 2); break;
+        case 6: if (bk == 64) XRS_GLDS(64, 80, 4, 1, 2, 64); else if (st4) XRS_GLDS(64, 80, 4, 1, 2, 32, 4); else XRS_GLDS(64, 80, 4, 1, 2); break;
+        case 7: if (bk == 64) XRS_GLDS(80, 64, 1, 4, 2, 64); else if (st4) XRS_GLDS(80, 64, 1, 4, 2, 32, 4); else XRS_GLDS(80, 64, 1, 4, 2); break;
         case 8: XRS_GLDS(64, 80, 2, 1, 2); break;
         case 9: XRS_GLDS(80, 64, 1, 2, 2); break;
         case 10: XRS_GLDS(64, 64, 1, 1, 4); break;
