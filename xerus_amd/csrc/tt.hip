@@ -1169,17 +1169,19 @@ void dot_async(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
     if (h->dot_worker == nullptr) h->dot_worker = new DotWorker(h);
     xrs_handle_t c = h->dot_worker->child();
     c->prof_mask = h->prof_mask;   // (the parent's profiler collects the child's records at prof_end)
-    XRS_HIP(hipEventRecord(h->ev_dot, h->stream));
-    XRS_HIP(hipStreamWaitEvent(c->stream, h->ev_dot, 0));
-    XRS_HIP(hipStreamWaitEvent(c->side_stream[0], h->ev_dot, 0));
     // Gate (default; XRS_DOT_GATE=0: start at once): the product starts behind the Gram chains of the next
     // round on this handle (open_dot_gate, called by chain_pass), so that it fills the round's
     // factorisation phase -- one batched Cholesky launch on a few CUs -- instead of halving the chains'
-    // share of the chip. Anything that waits for the product opens the gate first.
+    // share of the chip. Anything that waits for the product opens the gate first -- then at the main
+    // stream's current point (the fork below is recorded in either case: a gate opened by a wait carries
+    // no event of its own).
     static const bool gate = [] {
         const char* e = std::getenv("XRS_DOT_GATE");
         return !(e && e[0] == '0');
     }();
+    XRS_HIP(hipEventRecord(h->ev_dot, h->stream));
+    XRS_HIP(hipStreamWaitEvent(c->stream, h->ev_dot, 0));
+    XRS_HIP(hipStreamWaitEvent(c->side_stream[0], h->ev_dot, 0));
     h->dot_worker->post(d, n, rx, X, ry, Y, gate);
     h->dot_pending = true;
     h->reader_pending = true;
