@@ -811,9 +811,7 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         const char* e = std::getenv("XRS_GLDS_BK");
         return e ? std::atoi(e) : 32;
     }();
-    // XRS_GLDS_BK=4: 32-deep steps in 4 stages (a 3-step DMA lead; experiment)
     const int bk = (bk_pref == 64 && K % 64 == 0 && (var == 4 || var == 6 || var == 7)) ? 64 : kGldsBK;
-    const bool st4 = bk_pref == 4 && (var == 4 || var == 6 || var == 7);
     // split-K: whole K-steps per slice, aiming at `target` workgroups
     const long tiles = ntiles(var);
     const int ksteps = K / bk;
@@ -831,9 +829,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
         case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
         case 3: XRS_GLDS(64, 64, 2, 2, 1); break;
-        case 4: if (bk == 64) XRS_GLDS(64, 64, 2, 2, 2, 64); else if (st4) XRS_GLDS(64, 64, 2, 2, 2, 32, 4); else XRS_GLDS(64, 64, 2, 2, 2); break;
-        case 6: if (bk == 64) XRS_GLDS(64, 80, 4, 1, 2, 64); else if (st4) XRS_GLDS(64, 80, 4, 1, 2, 32, 4); else XRS_GLDS(64, 80, 4, 1, 2); break;
-        case 7: if (bk == 64) XRS_GLDS(80, 64, 1, 4, 2, 64); else if (st4) XRS_GLDS(80, 64, 1, 4, 2, 32, 4); else XRS_GLDS(80, 64, 1, 4, 2); break;
+        case 4: if (bk == 64) XRS_GLDS(64, 64, 2, 2, 2, 64); else XRS_GLDS(64, 64, 2, 2, 2); break;
+        case 6: if (bk == 64) XRS_GLDS(64, 80, 4, 1, 2, 64); else XRS_GLDS(64, 80, 4, 1, 2); break;
+        case 7: if (bk == 64) XRS_GLDS(80, 64, 1, 4, 2, 64); else XRS_GLDS(80, 64, 1, 4, 2); break;
         case 8: XRS_GLDS(64, 80, 2, 1, 2); break;
         case 9: XRS_GLDS(80, 64, 1, 2, 2); break;
         case 10: XRS_GLDS(64, 64, 1, 1, 4); break;
