@@ -76,7 +76,7 @@ def random_cores(xe, dims, ranks, seed):
 
 
 def load_traffic():
-    """HBM bytes per k_gemm_f64 launch from the committed rocprofv3 PMC pass of this bench (or None)."""
+    """HBM bytes per GEMM launch from the committed rocprofv3 PMC pass of this bench (or None)."""
     p = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
     if not os.path.exists(p):
         return None

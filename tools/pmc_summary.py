@@ -1,6 +1,6 @@
 """Summarise the PMC passes of tools/pmc_bench.sh per kernel family and write profiles/<tag>/pmc_*.
 
-HBM traffic per k_gemm_f64 launch = 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 derived counters, KiB).
+HBM traffic per GEMM launch (k_gemm_glds and k_gemm_f64 dispatches pooled) = calibrated FETCH_SIZE + WRITE_SIZE (rocprofv3 derived counters, KiB).
 MI355X_MICROARCH.md (HBM section): FETCH_SIZE reads exactly half of a 16-B/lane streaming read on gfx950;
 the 8-B/lane loads and stores of our kernels are calibrated by tools/fetch_calib.hip (pass "calf"/"calw"
 in the source directory): the factors measured there (FETCH x2 for 8-B and 16-B loads, WRITE x1 for 8-B
@@ -47,7 +47,16 @@ for p in ("fetch", "write", "mfma"):
             summary.setdefault(fam, {})[c] = {"dispatches": len(v), "mean": sum(v) / len(v)}
 with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
     json.dump(summary, f, indent=1, sort_keys=True)
-g = summary.get("xrs::k_gemm_f64", {})
+# the GEMM family: every GEMM kernel of the step (k_gemm_f64: general tiles; k_gemm_glds: LDS-DMA pipeline),
+# pooled per dispatch
+g = {}
+for p_ in ("fetch", "write", "mfma"):
+    for fam, counters in load(p_).items():
+        if not fam.startswith("xrs::k_gemm"):
+            continue
+        for c, v in counters.items():
+            g.setdefault(c, []).extend(v)
+g = {c: {"dispatches": len(v), "mean": sum(v) / len(v)} for c, v in g.items()}
 if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
     ff = cal["fetch"] or 1.0
     wf = cal["write"] or 1.0
@@ -61,7 +70,7 @@ if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
         "calibration": {"fetch_factor": ff, "write_factor": wf, "measured": cal.get("factors", {})},
         "dispatches": g["FETCH_SIZE"]["dispatches"],
         "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py --no-cpu --no-cfg5 --no-extras "
-                  "--steps 3 --warmup 1, mean per k_gemm_f64 dispatch, corrected by the 8-B load/store calibration of "
+                  "--steps 3 --warmup 1, mean per GEMM dispatch (k_gemm_glds + k_gemm_f64), corrected by the 8-B load/store calibration of "
                   "tools/fetch_calib.hip (FETCH x%.3f, WRITE x%.3f); %s/pmc_summary.json" % (ff, wf, dst),
     }
     if "SQ_VALU_MFMA_BUSY_CYCLES" in g and "GRBM_GUI_ACTIVE" in g:
@@ -71,4 +80,4 @@ if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 else:
-    print("no k_gemm_f64 FETCH/WRITE data:", list(summary))
+    print("no GEMM FETCH/WRITE data:", list(summary))
