@@ -269,8 +269,8 @@ template <int K>
 __device__ __forceinline__ double row_bcast_d(double v) {
     union { double d; int i[2]; } u;
     u.d = v;
-    u.i[0] = __builtin_amdgcn_update_dpp(0, u.i[0], 0x150 + K, 0xF, 0xF, false);
-    u.i[1] = __builtin_amdgcn_update_dpp(0, u.i[1], 0x150 + K, 0xF, 0xF, false);
+    u.i[0] = __builtin_amdgcn_mov_dpp(u.i[0], 0x150 + K, 0xF, 0xF, false);   // (every lane has a source:
+    u.i[1] = __builtin_amdgcn_mov_dpp(u.i[1], 0x150 + K, 0xF, 0xF, false);   //  no zero-initialised "old")
     return u.d;
 }
 

@@ -27,12 +27,23 @@ namespace {
 constexpr int SV_LDS = 18432;   // doubles (144 KiB)
 constexpr int SV_MAXP = 512;
 
-// DPP move of a double (two 32-bit moves); CTRL is a DPP16 control word
+// DPP move of a double (two 32-bit moves); CTRL is a DPP16 control word whose every lane has a valid
+// source (row rotations / mirrors / quad permutations), so no "old" value is needed (mov_dpp: no
+// zero-initialised destination, which update_dpp(0, ...) costs two extra moves per double)
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
+}
+
+// The value of lane l ^ 16 (the other DPP row of a 32-lane group) by gfx950's v_permlane16_swap (a VALU
+// exchange of odd and even 16-lane rows; __shfl_xor goes through the LDS crossbar)
+__device__ __forceinline__ double xor16(double v) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    // odd rows receive the even rows in the first result, even rows the odd rows in the second
+    return (threadIdx.x & 16) ? __hiloint2double(hi[0], lo[0]) : __hiloint2double(hi[1], lo[1]);
 }
 
 // Sum over a group of G (8, 16 or 32) consecutive lanes. Every lane of the group ends with the same bits:
@@ -46,7 +57,7 @@ __device__ __forceinline__ double gsum(double v) {
         v += dpp<0x124>(v);
         v += dpp<0x122>(v);
         v += dpp<0x121>(v);
-        if constexpr (G == 32) v += __shfl_xor(v, 16, 64);   // the two DPP rows of the group
+        if constexpr (G == 32) v += xor16(v);   // the two DPP rows of the group
     } else {
         static_assert(G == 8, "groups of 8 or 16 lanes");
         v += dpp<0x141>(v);
