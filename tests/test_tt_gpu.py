@@ -358,3 +358,34 @@ def test_paired_chain_launches(handle, ref, monkeypatch):
         gx.free()
         gy.free()
     assert abs(results["0"] - results["1"]) <= 1e-13 * nx * ny
+
+
+@pytest.mark.parametrize("edge", [None, 1])
+def test_dot_async_beside_fallback_round(handle, ref, edge):
+    """x.dot_async(y) before a round whose first certificate fails (x + x: doubled ranks; or a
+    rank-deficient interior core): the round falls back (truncating / sequential paths), which open the
+    product's gate at their own chain pass or at the first release; the product is still the one of the
+    pre-round x and the round is the reference's."""
+    rng = ref.Rng(23)
+    if edge is None:
+        x0 = ref.TT.random([5, 4, 6, 3, 5], [4, 7, 6, 3], rng)
+        x = ref.tt_add(x0, x0)
+        target = 100
+    else:
+        x = ref.TT.random_raw([5, 5, 5, 5, 5], [4, 6, 6, 4], rng)
+        c = x.cores[edge]
+        U, S, Vt = np.linalg.svd(c.reshape(c.shape[0], -1), full_matrices=False)
+        S[2:] = 0.0
+        x.cores[edge] = ((U * S) @ Vt).reshape(c.shape)
+        target = 6
+    y = ref.TT.random_raw(x.dims, x.ranks, rng)
+    gx = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    gy = capi.TTDevice.from_cores(handle, y.cores)
+    d_ref = ref.dot(x, y)
+    nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
+    fut = gx.dot_async(gy)
+    gx.round(target)
+    assert abs(fut.result() - d_ref) <= 1e-12 * nx * ny
+    ox = x.copy()
+    ox.round(target)
+    assert gx.ranks == ox.ranks
