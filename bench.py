@@ -456,7 +456,7 @@ def main():
         traffic = load_traffic()
         roofline = {
             "bound": "mfma",
-            "kernel": "k_gemm_f64 (all GEMM launches of the step, fp64 MFMA 16x16x4)",
+            "kernel": "GEMM family: k_gemm_glds (LDS-DMA pipeline) + k_gemm_f64 (general tiles), every GEMM launch of the step, fp64 MFMA 16x16x4",
             "achieved": round(gemm_tflops, 3),
             "peak": FP64_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
