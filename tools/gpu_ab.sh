@@ -1,12 +1,12 @@
 #!/bin/bash
-# A/B of one environment switch: GEMM + TT parity under $AB, then the headline step twice
+# A/B of one environment switch: GEMM + TT parity under $TESTENV (default: the default code), then the headline step twice
 # each way (default, $AB) alternating, and a kernel trace of the default step.
 # Usage: AB="XRS_REDUCE_V1=1" bash tools/gpu_ab.sh
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 B="python bench.py --no-cpu --no-cfg5 --no-extras --steps 30 --warmup 5"
-env $AB timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_tt_gpu.py -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 \
+env $TESTENV timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_tt_gpu.py tests/test_cfg5_gpu.py tests/test_reference_ports_gpu.py -q -m gpu -x --timeout 120 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 \
   && tail -1 gpurun_out/ab_tests.log \
   && timeout -k 10 120 $B > gpurun_out/ab_def1.json \
   && env $AB timeout -k 10 120 $B > gpurun_out/ab_alt1.json \
