@@ -816,7 +816,26 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
     const long tiles = ntiles(var);
     const int ksteps = K / bk;
     int splits = 1;
-    if (tiles < g_target) splits = int(std::min<long>((g_target + tiles - 1) / tiles, std::max(1, ksteps * bk / 128)));
+    static const bool split_old = std::getenv("XRS_GLDS_SPLIT_OLD") != nullptr;   // (A/B: the plain target rule)
+    if (tiles < g_target && split_old) {
+        splits = int(std::min<long>((g_target + tiles - 1) / tiles, std::max(1, ksteps * bk / 128)));
+    } else if (tiles < g_target) {
+        // Whole waves of workgroups: the launch takes rounds(s) x ceil(ksteps / s) K-steps per CU, where
+        // rounds(s) = ceil(tiles s / resident) and resident = target x the workgroups one CU holds (LDS
+        // stages of 96-128 KB: one; the 32x32 tile: three). Picking s by the target alone overshoots into a
+        // second, mostly idle round (the 6 orthogonality Grams of the bench round: 60 tiles x 5 slices =
+        // 300 workgroups on 256 CUs, 64 K-steps per CU, against 40 at 4 slices).
+        const int nwaves = (var == 4 || var == 6 || var == 7) ? 8 : 4;
+        const int lds_kb = (bk == 64 ? 2 : 3) * (bms[var] + bns[var]) * bk * 8 / 1024;
+        const long resident = long(g_target) * std::max(1, std::min(160 / lds_kb, 16 / nwaves));
+        const int smax = std::max(1, ksteps * bk / 128);
+        long best = -1;
+        for (int s = 1; s <= smax; ++s) {
+            const int steps = (ksteps + s - 1) / s, seff = (ksteps + steps - 1) / steps;
+            const long cost = (tiles * seff + resident - 1) / resident * steps;
+            if (best < 0 || cost < best) best = cost, splits = seff;
+        }
+    }
     int kps = (ksteps + splits - 1) / splits * bk;
     splits = (K + kps - 1) / kps;
     DevBuf slab;
