@@ -310,6 +310,32 @@ def bench_svd(h):
     return out
 
 
+def host_cpu_info():
+    """nproc, the CPUs this process may run on, the CPU model, and the thread count of the all-cores leg
+    (the job's CPU share: OMP_NUM_THREADS when the launcher sets it -- 16 per GPU on the GPU box, where
+    nproc shows the whole machine -- else the affinity mask)."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        threads, rule = min(int(env), affinity), "min(OMP_NUM_THREADS, affinity)"
+    else:
+        threads, rule = affinity, "affinity mask"
+    return {"nproc": nproc, "affinity": affinity, "model": model, "threads": max(1, threads), "rule": rule}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -486,28 +512,45 @@ def main():
                 from threadpoolctl import threadpool_limits
             except ImportError:
                 threadpool_limits = None
-            xo, yo = ref.TT([c.copy() for c in xc]), ref.TT([c.copy() for c in yc])
-            xo.move_core(0)
-            yo.move_core(0)
-            ctx = threadpool_limits(limits=1) if threadpool_limits else None
-            if ctx:
-                ctx.__enter__()
-            t_c = time.perf_counter()
-            for _ in range(args.cpu_steps):
-                ref.dot(xo, yo)
-                xo.round(r)
-            t_c = time.perf_counter() - t_c
-            if ctx:
-                ctx.__exit__(None, None, None)
+            def cpu_leg(threads, steps):
+                xo, yo = ref.TT([c.copy() for c in xc]), ref.TT([c.copy() for c in yc])
+                xo.move_core(0)
+                yo.move_core(0)
+                ctx = threadpool_limits(limits=threads) if threadpool_limits else None
+                if ctx:
+                    ctx.__enter__()
+                try:
+                    t0 = time.perf_counter()
+                    for _ in range(steps):
+                        ref.dot(xo, yo)
+                        xo.round(r)
+                    return time.perf_counter() - t0
+                finally:
+                    if ctx:
+                        ctx.__exit__(None, None, None)
+
+            host = host_cpu_info()
+            t_1 = cpu_leg(1, args.cpu_steps)
+            t_all = cpu_leg(host["threads"], args.cpu_steps)
+            sample = (f"{args.cpu_steps} full steps (<x,y> + round({r})) of the same order-{d} n={n} r={r} workload and "
+                      f"inputs, numpy/scipy-LAPACK restatement of the reference (dgeqp3/dorgqr/dgesdd/dgemm call sequence)")
             cpu = {
-                "value": round(f_step * args.cpu_steps / t_c / 1e9, 3),
+                "value": round(f_step * args.cpu_steps / t_all / 1e9, 3),
                 "unit": "GFLOP/s",
-                "cores": 1,
+                "cores": host["threads"],
                 "kind": "port",
-                "sample": f"{args.cpu_steps} full steps (<x,y> + round({r})) of the same order-{d} n={n} r={r} "
-                          f"workload and inputs, numpy/scipy-LAPACK restatement of the reference "
-                          f"(dgeqp3/dorgqr/dgesdd/dgemm call sequence), 1 BLAS thread, {t_c:.2f} s",
-                "ms_per_step": round(t_c / args.cpu_steps * 1e3, 2),
+                "sample": f"{sample}, {host['threads']} BLAS threads (all cores this job may use), {t_all:.2f} s",
+                "ms_per_step": round(t_all / args.cpu_steps * 1e3, 2),
+                "single_core": {
+                    "value": round(f_step * args.cpu_steps / t_1 / 1e9, 3),
+                    "cores": 1,
+                    "ms_per_step": round(t_1 / args.cpu_steps * 1e3, 2),
+                    "sample": f"{sample}, 1 BLAS thread, {t_1:.2f} s",
+                },
+                "nproc": host["nproc"],
+                "affinity_cpus": host["affinity"],
+                "cpu_model": host["model"],
+                "threads_rule": host["rule"],
             }
         out = {
             "metric": "GFLOP/s on TT contraction + TT-round sweep time, order-10 rank-256",

@@ -3,6 +3,7 @@
 #include "xerus/basic.h"
 #include "xerus/index.h"
 #include "xerus/indexedTensor.h"
+#include "xerus/indexedTensor_tensor_factorisations.h"
 #include "xerus/misc/fileIO.h"
 #include "xerus/misc/random.h"
 #include "xerus/tensor.h"

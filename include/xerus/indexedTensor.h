@@ -98,6 +98,8 @@ namespace internal {
 /// Evaluates a product into a tensor whose modes follow `_out` (LHS indices; resolved against the
 /// product's open degree). Used by the assignment operators.
 Tensor evaluate_product(const IndexedProduct& _p, const std::vector<Index>& _out);
+/// spans resolved against a tensor of the given degree (index.cpp:64-92), span-0 indices dropped
+std::vector<Index> resolve_indices(const std::vector<Index>& _indices, size_t _degree);
 }  // namespace internal
 
 }  // namespace xerus

@@ -77,6 +77,10 @@ class TTTensor {
     void round(const size_t _maxRank);
     void round(const int _maxRank);
     void round(const value_t _eps);
+    /// TTNetwork::soft_threshold (ttNetwork.cpp:688-713): per edge sigma -> max(0, sigma - tau);
+    /// _taus[0] applies to the last edge, as in the reference; _preventZero is unused there too
+    void soft_threshold(const std::vector<double>& _taus, const bool _preventZero = false);
+    void soft_threshold(const double _tau, const bool _preventZero = false);
 
     value_t frob_norm() const;
 

@@ -129,12 +129,14 @@ int xrs_svd(xrs_handle_t handle, double* U, double* S, double* Vt, const double*
 /** Solve A X = B, A m x n, B m x p, X n x p (replaces blasWrapper::solve, blasLapackWrapper.cpp:540-640):
  *  the reference's dispatch (m != n: least squares; not symmetric: general; symmetric with a positive
  *  diagonal: Cholesky, falling back to the general path). Cholesky is blocked (any n); the general and
- *  least-squares paths are the SVD solve of xrs_solve_least_squares (min(m, n) <= 512). Synchronises. */
+ *  least-squares paths are the solve of xrs_solve_least_squares. Synchronises. */
 int xrs_solve(xrs_handle_t handle, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
 /** Minimum-norm least-squares solution of A X = B (replaces blasWrapper::solve_least_squares / dgelsd,
- *  blasLapackWrapper.cpp:647-721): X = V S^+ U^T B, singular values <= EPSILON * sigma_max dropped. */
+ *  blasLapackWrapper.cpp:647-721): X = V S^+ U^T B, singular values <= EPSILON * sigma_max dropped
+ *  (min(m, n) <= 512); above, a shifted-CholeskyQR3 QR / LQ solve for full-rank A (rank-deficient A of
+ *  that size: XRS_ENUMERIC). */
 int xrs_solve_least_squares(xrs_handle_t handle, double* X, const double* A, size_t m, size_t n, const double* B, size_t p);
-/** Singular values and right singular vectors of the rows of A (p x q, p <= q <= 512) by one-sided
+/** Singular values and right singular vectors of the rows of A (p x q, p <= q <= 1024; kernel 1: p <= 512) by one-sided
  *  Jacobi -- the SVD step of the truncating TT round (TTNetwork::round's per-edge svd,
  *  ttNetwork.cpp:644-665, without U). S: p descending; Vt: p x q, orthonormal rows for S > 0.
  *  kernel: 0 auto, 1 one workgroup, 2 multi-workgroup blocks (p > 16). *sweeps (host): Jacobi
@@ -157,6 +159,12 @@ int xrs_tt_move_core(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, 
  *  sigma_j <= eps*sigma_0 (tensor.cpp:1463-1474). On return the core is at position 0. */
 int xrs_tt_round(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
                  int canonicalized, size_t core_position, const size_t* max_ranks, double eps);
+/** TTNetwork::soft_threshold (ttNetwork.cpp:688-713): left-to-right QC sweep (canonicalize_right), then
+ *  right to left per edge the SVD with no rank cut beyond exact zeros (maxRank = inf, eps = 0) whose
+ *  singular values become max(0, sigma - tau) (round_edge's _softThreshold, tensorNetwork.cpp:766,788).
+ *  taus: d-1 thresholds, taus[0] for the LAST edge (the reference's loop order). Core ends at 0. */
+int xrs_tt_soft_threshold(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
+                          int canonicalized, size_t core_position, const double* taus);
 /** TTOperator application, the core-wise contraction of a TTStack (ttStack.cpp:197-309, built by
  *  TTNetwork<true>::specialized_contraction_f, ttNetwork.cpp:886-967). Operator A: cores
  *  (ra[k], n[k], m[k], ra[k+1]). With p == NULL, B is a TTTensor with cores (rb[k], m[k], rb[k+1]) and

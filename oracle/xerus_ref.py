@@ -301,7 +301,8 @@ class TT:
 
     # ---- round_edge (tensorNetwork.cpp:678-818) for TT: from = right core (fromPos = 0, transFrom),
     #      to = left core (toPos = last, transTo)
-    def round_edge(self, frm: int, to: int, max_rank: int, eps: float):
+    def round_edge(self, frm: int, to: int, max_rank: int, eps: float, soft: float = 0.0):
+        """soft > 0: the kept singular values become max(0, sigma - soft) (:766, :788)."""
         F = self.cores[frm]          # (b, n, c)
         T = self.cores[to]           # (a, n', b)
         b = F.shape[0]
@@ -311,7 +312,7 @@ class TT:
             X = coreA.T @ coreB.T                         # contract(X, coreA, true, coreB, true, 1) (:761)
             U, S, Vt = svd(X)                             # (:764)
             k = svd_rank(S, max_rank, eps)
-            U, S, Vt = U[:, :k], S[:k], Vt[:k, :]
+            U, S, Vt = U[:, :k], np.maximum(0.0, S[:k] - soft), Vt[:k, :]
             coreB = S[:, None] * Vt                       # (:769)
             self.cores[frm] = (U.T @ Qf).reshape(k, F.shape[1], F.shape[2])           # (:773)
             self.cores[to] = (Qt @ coreB.T).reshape(T.shape[0], T.shape[1], k)        # (:779)
@@ -319,7 +320,7 @@ class TT:
             X = F.reshape(b, -1).T @ T.reshape(-1, b).T   # (n c) x (a n') (:783)
             U, S, Vt = svd(X)
             k = svd_rank(S, max_rank, eps)
-            U, S, Vt = U[:, :k], S[:k], Vt[:k, :]
+            U, S, Vt = U[:, :k], np.maximum(0.0, S[:k] - soft), Vt[:k, :]
             self.cores[to] = (Vt.T * S[None, :]).reshape(T.shape[0], T.shape[1], k)   # (:790-791)
             self.cores[frm] = np.ascontiguousarray(U.T).reshape(k, F.shape[1], F.shape[2])  # (:797-802)
 
@@ -332,6 +333,22 @@ class TT:
         self.move_core(d - 1)
         for i in range(d - 1):
             self.round_edge(d - 1 - i, d - 2 - i, max_ranks[d - 2 - i], eps)
+        self.core_position = 0
+        self.canonicalized = True
+        if init_canon:
+            self.move_core(init_pos)
+
+    def soft_threshold(self, taus):
+        """TTNetwork::soft_threshold (ttNetwork.cpp:688-713): canonicalize_right, then
+        round_edge(numComponents - i, numComponents - i - 1, max, 0.0, taus[i]) -- taus[0] at the LAST edge."""
+        d = self.order
+        if isinstance(taus, (int, float, np.floating)):
+            taus = [float(taus)] * (d - 1)
+        assert len(taus) == d - 1
+        init_canon, init_pos = self.canonicalized, self.core_position
+        self.move_core(d - 1)
+        for i in range(d - 1):
+            self.round_edge(d - 1 - i, d - 2 - i, 2 ** 62, 0.0, taus[i])
         self.core_position = 0
         self.canonicalized = True
         if init_canon:

@@ -115,6 +115,20 @@ def test_solve_general_and_least_squares(xe, m, n):
     assert _rel(X2, want) <= 1e-10
 
 
+@pytest.mark.parametrize("m,n", [(600, 600), (700, 560), (560, 700)])
+def test_solve_general_above_512(xe, m, n):
+    """min(m, n) > 512: nonsymmetric square, tall least-squares and wide minimum-norm systems through the
+    shifted-CholeskyQR3 QR / LQ solve (the reference: dgesv / dgelsd, no size limit)."""
+    rng = np.random.default_rng(m * 7 + n)
+    M = rng.standard_normal((m, n))
+    B = rng.standard_normal((m, 3))
+    want = np.linalg.lstsq(M, B, rcond=None)[0]
+    X = xe.solve(_tensor(xe, M), _tensor(xe, B), 1).to_ndarray()
+    assert _rel(X, want) <= 1e-9
+    X2 = xe.solve_least_squares(_tensor(xe, M), _tensor(xe, B), 1).to_ndarray()
+    assert _rel(X2, want) <= 1e-9
+
+
 def test_solve_tensor_modes(xe):
     """A (i, j, k, l) X (k, l) = B (i, j): the leading B.degree() modes of A are contracted (tensor.cpp:1654)."""
     rng = np.random.default_rng(2)

@@ -125,3 +125,50 @@ def test_tt_dot_generic_network_order12(xe, ref):
     zip_ = xe.dot(tx, ty)
     assert abs(net - want) <= 1e-12 * nx * ny
     assert abs(zip_ - want) <= 1e-12 * nx * ny
+
+
+def _approx(a, b, eps=4 * np.finfo(float).eps):
+    """misc::approx_equal (include/xerus/misc/math.h:71-73)."""
+    return abs(a - b) <= eps * 0.5 * (abs(a) + abs(b))
+
+
+def test_contractions_of_4_to_degree_0(xe):
+    """TensorNetwork:contractions_of_4_to_degree_0 (tensorNetwork.cxx:27-46): the ring A-D, B-C closed over
+    two size-1 links contracts to (A.D)(B.C) in every factor order, to 1e-20 (the same contraction order
+    is found whatever order the factors are written in)."""
+    xe.seed(0xBAADF00D)
+    A, B, C, D = (xe.Tensor.random([100, 1]) for _ in range(4))
+    E = xe.Tensor()
+    i1, i2, i3, i4 = xe.indices(4)
+    E() << A(i1, i2) * D(i1, i2)
+    a1 = E[0]
+    E() << B(i3, i4) * C(i3, i4)
+    a2 = E[0]
+    E() << A(i1, i2) * B(i3, i2) * C(i3, i4) * D(i1, i4)
+    assert _approx(E[0], a1 * a2, 1e-20)
+    E() << B(i3, i2) * C(i3, i4) * D(i1, i4) * A(i1, i2)
+    assert _approx(E[0], a1 * a2, 1e-20)
+    E() << B(i3, i2) * D(i1, i4) * C(i3, i4) * A(i1, i2)
+    assert _approx(E[0], a1 * a2, 1e-20)
+
+
+def test_contractions_of_3_to_degree_0(xe):
+    """TensorNetwork:contractions_of_3_to_degree_0 (tensorNetwork.cxx:48-66): a closed 3-ring in three
+    factor orders (the 3-node closed-form order, tensorNetwork.cpp:1269-1313), equal to 4 eps."""
+    xe.seed(0xBAADF00D)
+    A = xe.Tensor.random([1, 10])
+    B = xe.Tensor.random([10, 100])
+    C = xe.Tensor.random([100, 1])
+    assert B.is_dense()
+    E = xe.Tensor()
+    i1, i2, i3 = xe.indices(3)
+    E() << A(i1, i2) * B(i2, i3) * C(i3, i1)
+    a1 = E[0]
+    E() << B(i2, i3) * C(i3, i1) * A(i1, i2)
+    a2 = E[0]
+    E() << C(i3, i1) * B(i2, i3) * A(i1, i2)
+    a3 = E[0]
+    assert _approx(a1, a2)
+    assert _approx(a2, a3)
+    want = float((A.to_ndarray() @ B.to_ndarray() @ C.to_ndarray())[0, 0])
+    assert abs(a1 - want) <= 1e-13 * np.sqrt(100 * 10)

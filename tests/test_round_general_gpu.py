@@ -1,0 +1,96 @@
+"""The truncating TT round on inputs the certified paths refuse, at BASELINE cfg3 size (order 10, n = 20,
+r = 128), against the oracle (the reference's two-sweep algorithm on LAPACK, oracle/xerus_ref.py:
+TTNetwork::round ttNetwork.cpp:644-684 -> round_edge tensorNetwork.cpp:678-818).
+
+Inputs (seeded):
+  graded  -- raw N(0,1) cores whose right rank index is scaled by 0.8^j: every edge unfolding has a
+             decaying spectrum (kappa ~ 1e12 at the rank-128 edges), so no Gram-based certificate holds;
+  sum     -- x + 1e-6 y with x, y random rank-128 TTs (rank 256, a 1e-6 tail).
+Bars (BASELINE.md §3 / SURVEY §8(d)): identical ranks; truncation errors agree to 1e-6 ||x||. The
+round's path is asserted so that these tests pin the general (non-certified) algorithm.
+"""
+import numpy as np
+import pytest
+
+from xerus_amd import capi
+
+pytestmark = pytest.mark.gpu
+
+EPSILON = 8 * np.finfo(float).eps
+
+
+def graded_tt(ref, dims, ranks, decay, seed):
+    x = ref.TT.random_raw(dims, ranks, ref.Rng(seed))
+    for k in range(len(dims) - 1):
+        b = x.cores[k].shape[2]
+        x.cores[k] = x.cores[k] * (decay ** np.arange(b))[None, None, :]
+    return x
+
+
+def sum_tt(ref, dims, ranks, scale, seed):
+    rng = ref.Rng(seed)
+    x = ref.TT.random(dims, ranks, rng)
+    y = ref.TT.random(dims, ranks, rng)
+    y.cores[0] = y.cores[0] * scale
+    return ref.tt_add(x, y)
+
+
+def _check(handle, ref, x, max_ranks, eps, allowed_paths):
+    from ttutil import tt_diff_norm
+
+    g = capi.TTDevice.from_cores(handle, [c.copy() for c in x.cores])
+    g.round(max_ranks, eps)
+    path = handle.last_round_path()
+    o = x.copy()
+    o.round(max_ranks, eps)
+    assert g.ranks == o.ranks, (g.ranks, o.ranks, path)
+    e_gpu, nrm = tt_diff_norm(g.cores(), x.cores)
+    e_ref, _ = tt_diff_norm(o.cores, x.cores)
+    assert abs(e_gpu - e_ref) <= 1e-6 * nrm, (e_gpu / nrm, e_ref / nrm, path)
+    assert path in allowed_paths, path
+    for c in g.cores()[1:]:   # right-canonical result (core at 0)
+        M = c.reshape(c.shape[0], -1)
+        assert np.abs(M @ M.T - np.eye(M.shape[0])).max() <= 1e-10
+    return g, o, path
+
+
+CFG3 = ([20] * 10, [128] * 9)
+
+
+def test_graded_round64(handle, ref):
+    """round(64) of a graded-spectrum TT at cfg3 size: the maxRank cut on a decaying spectrum."""
+    x = graded_tt(ref, *CFG3, decay=0.8, seed=101)
+    _check(handle, ref, x, [64] * 9, EPSILON, ("general", "reference"))
+
+
+def test_graded_round_eps(handle, ref):
+    """round(1e-8) (eps only, maxRank = inf) of the graded TT: the eps rule sigma_j <= 1e-8 sigma_0 decides
+    every rank; the singular values near the cut must be accurate to far better than sqrt(u)."""
+    x = graded_tt(ref, *CFG3, decay=0.8, seed=102)
+    g, o, _ = _check(handle, ref, x, [2 ** 62] * 9, 1e-8, ("general", "reference"))
+    assert max(o.ranks) < 128   # the eps rule did cut
+
+
+def test_sum_round64(handle, ref):
+    """round(64) of x + 1e-6 y (ranks 256 with a 1e-6 tail at cfg3 size)."""
+    x = sum_tt(ref, *CFG3, scale=1e-6, seed=103)
+    _check(handle, ref, x, [64] * 9, EPSILON, ("general", "reference", "truncate"))
+
+
+def test_sum_round_eps(handle, ref):
+    """round(1e-7) of x + 1e-6 y: the eps rule removes y's contribution edge by edge."""
+    x = sum_tt(ref, *CFG3, scale=1e-9, seed=104)
+    g, o, _ = _check(handle, ref, x, [2 ** 62] * 9, 1e-7, ("general", "reference"))
+    assert o.ranks == [20] + [128] * 7 + [20]
+
+
+@pytest.mark.parametrize("dims,ranks,max_rank,eps", [
+    ([4, 5, 3, 4, 2], [3, 6, 5, 2], 3, 1e-3),
+    ([6] * 6, [20] * 5, 9, 1e-10),
+    ([20] * 6, [40] * 5, 100, 1e-6),
+    ([3] * 8, [9] * 7, 4, EPSILON),
+])
+def test_graded_small(handle, ref, dims, ranks, max_rank, eps):
+    """Small graded TTs (boundary ranks, tall and wide edges, maxRank and eps cuts together)."""
+    x = graded_tt(ref, dims, ranks, decay=0.7, seed=105 + len(dims))
+    _check(handle, ref, x, [max_rank] * (len(dims) - 1), eps, ("general", "reference", "truncate", "chain"))

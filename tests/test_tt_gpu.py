@@ -93,6 +93,39 @@ def test_dot_async_beside_round(handle, ref, dims, ranks):
         capi._check("xrs_tt_dot_wait", handle.lib.xrs_tt_dot_wait(handle.h, capi.C.byref(capi.C.c_double())))
 
 
+@pytest.mark.parametrize("write", ["scal", "axpy", "copy", "upload", "gemm"])
+def test_dot_async_fences_in_place_writes(handle, ref, write):
+    """x.dot_async(y), then an in-place write into one of x's live cores through the C-ABI: the write
+    waits for the in-flight product (fence_readers), so result() is the pre-write <x,y>."""
+    rng = ref.Rng(31)
+    dims, ranks = [20] * 8, [64] * 7
+    x = ref.TT.random_raw(dims, ranks, rng)
+    y = ref.TT.random_raw(dims, ranks, rng)
+    gx = capi.TTDevice.from_cores(handle, x.cores)
+    gy = capi.TTDevice.from_cores(handle, y.cores)
+    d_before = gx.dot(gy)
+    k = 3
+    size = gx.r[k] * gx.dims[k] * gx.r[k + 1]
+    core = capi.DeviceArray(handle, (size,), ptr=gx.ptrs[k], owned=False)
+    other = handle.array(np.full(size, 0.5))
+    fut = gx.dot_async(gy)
+    if write == "scal":
+        handle.scal(core, -3.0)
+    elif write == "axpy":
+        handle.axpy(core, 2.0, other)
+    elif write == "copy":
+        capi._check("xrs_copy", handle.lib.xrs_copy(handle.h, capi._DP(core.ptr), capi._DP(other.ptr), size))
+    elif write == "upload":
+        z = np.zeros(size)
+        capi._check("xrs_upload", handle.lib.xrs_upload(handle.h, capi._DP(core.ptr), z.ctypes.data_as(capi._DP), size))
+    else:
+        a = handle.array(np.eye(gx.r[k]))
+        b = handle.array(np.ones((gx.r[k], gx.dims[k] * gx.r[k + 1])))
+        handle.gemm(core, gx.r[k], gx.dims[k] * gx.r[k + 1], 1.0, a, gx.r[k], False, gx.r[k], b, gx.dims[k] * gx.r[k + 1], False)
+    assert fut.result() == d_before
+    assert gx.dot(gy) != d_before   # the write did happen
+
+
 @pytest.mark.parametrize("dims,ranks", [([4, 5, 3, 4, 2], [3, 6, 5, 2]), ([3, 3, 3, 3], [9, 9, 9]),
                                         ([20] * 6, [40] * 5), ([20] * 8, [128] * 7)])
 def test_random_move_core_left(handle, ref, dims, ranks):

@@ -68,6 +68,8 @@ SIGNATURES = {
     "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                      C.POINTER(_SZ), C.POINTER(_DP), _DP, _DP]),
     "xrs_tt_last_round_path": (C.c_int, [_DP]),
+    "xrs_tt_soft_threshold": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ,
+                                        C.POINTER(C.c_double)]),
     "xrs_comm_unique_id": (C.c_int, [_DP]),
     "xrs_comm_create": (C.c_int, [_DP, C.c_int, C.c_int, _DP, C.POINTER(_DP)]),
     "xrs_comm_destroy": (C.c_int, [_DP]),
@@ -471,6 +473,19 @@ class TTDevice:
                                           mr, eps)
         self._writeback(r, cores)
         _check("xrs_tt_round", st)
+        self.canonicalized, self.core_position = True, 0
+
+    def soft_threshold(self, taus):
+        """TTNetwork::soft_threshold (xrs_tt_soft_threshold): taus[0] applies to the LAST edge."""
+        d = self.order
+        if isinstance(taus, (int, float)):
+            taus = [float(taus)] * (d - 1)
+        n, r, cores = self._arrays()
+        t = (C.c_double * max(1, d - 1))(*taus)
+        st = self.handle.lib.xrs_tt_soft_threshold(self.handle.h, d, n, r, cores, int(self.canonicalized),
+                                                   self.core_position, t)
+        self._writeback(r, cores)
+        _check("xrs_tt_soft_threshold", st)
         self.canonicalized, self.core_position = True, 0
 
     def dot(self, other: "TTDevice") -> float:

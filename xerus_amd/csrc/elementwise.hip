@@ -278,6 +278,7 @@ int xrs_asum(xrs_handle_t h, double* result, const double* x, size_t n) {
 int xrs_scal(xrs_handle_t h, double* x, double alpha, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && (n == 0 || x), "null argument");
+        fence_readers(h);
         scal(h, x, alpha, n);
     });
 }
@@ -285,6 +286,7 @@ int xrs_scal(xrs_handle_t h, double* x, double alpha, size_t n) {
 int xrs_axpy(xrs_handle_t h, double* y, double alpha, const double* x, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && (n == 0 || (x && y)), "null argument");
+        fence_readers(h);
         axpy(h, y, alpha, x, n);
     });
 }
@@ -292,6 +294,7 @@ int xrs_axpy(xrs_handle_t h, double* y, double alpha, const double* x, size_t n)
 int xrs_scale_rows(xrs_handle_t h, double* X, const double* s, size_t m, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && (m * n == 0 || (X && s)), "null argument");
+        fence_readers(h);
         scale_rows(h, X, s, m, n);
     });
 }

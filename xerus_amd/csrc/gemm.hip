@@ -767,12 +767,13 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
 template <class PTR>
 static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int K, double alpha, size_t lda, bool ta,
                       size_t ldb, bool tb, bool sym, int tri) {
-    static int g_var = -1, g_target = 256;
-    static bool read = false;
-    if (!read) {
-        read = true;
-        if (const char* e = std::getenv("XRS_GEMM_GLDS")) std::sscanf(e, "%d,%d", &g_var, &g_target);
-    }
+    // (function-local static initialised once, thread-safe: the DotWorker thread runs GEMMs concurrently)
+    static const std::pair<int, int> g_env = [] {
+        int v = -1, t = 256;
+        if (const char* e = std::getenv("XRS_GEMM_GLDS")) std::sscanf(e, "%d,%d", &v, &t);
+        return std::make_pair(v, t);
+    }();
+    const int g_var = g_env.first, g_target = g_env.second;
     if (g_var == 0) return false;
     if (K % kGldsBK != 0 || (lda & 1) || (ldb & 1)) return false;
     for (int i = 0; i < count; ++i)
@@ -881,12 +882,13 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     //   v4  32x32  (8 waves 2x2, K split 2)   TT "wide"/"tall" shapes (M or N = r, other = n r)
     //   v8/v9: v3/v4 with a 4-deep ring; v10-v13: K-step 32 / 4-wave / 16-wave variants (tuning only)
     // split-K brings the grid to ~target workgroups while every split keeps >= kmin of K.
-    static int cfg_var = 0, cfg_kmin = 256, cfg_target = 512;
-    static bool cfg_read = false;
-    if (!cfg_read) {
-        cfg_read = true;
-        if (const char* e = std::getenv("XRS_GEMM_CFG")) std::sscanf(e, "%d,%d,%d", &cfg_var, &cfg_kmin, &cfg_target);
-    }
+    struct Cfg { int var = 0, kmin = 256, target = 512; };
+    static const Cfg g_cfg = [] {   // thread-safe one-time initialisation (concurrent DotWorker GEMMs)
+        Cfg c;
+        if (const char* e = std::getenv("XRS_GEMM_CFG")) std::sscanf(e, "%d,%d,%d", &c.var, &c.kmin, &c.target);
+        return c;
+    }();
+    const int cfg_var = g_cfg.var, cfg_kmin = g_cfg.kmin, cfg_target = g_cfg.target;
     // (batched: the tile counts are over the whole batch)
     auto ntiles = [&](int bm, int bn) { return long(count) * ((M + bm - 1) / bm) * ((N + bn - 1) / bn); };
     //   v14 64x80 / v15 80x64 (8 waves, K split 2, K-step 32): 256 x 5120 and 5120 x 256 TT shapes in
@@ -1162,6 +1164,7 @@ extern "C" int xrs_gemm(xrs_handle_t h, double* C, size_t M, size_t N, double al
         XRS_REQUIRE(transA ? lda >= M || K == 0 : lda >= K || M == 0, "lda too small");
         XRS_REQUIRE(transB ? ldb >= K || N == 0 : ldb >= N || K == 0, "ldb too small");
         XRS_REQUIRE(C != A && C != B, "C must not alias A or B");
+        xrs::fence_readers(h);
         xrs::gemm(h, C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
     });
 }
@@ -1180,6 +1183,7 @@ extern "C" int xrs_gemm_batched(xrs_handle_t h, size_t count, double* const* C, 
             XRS_REQUIRE(K == 0 || M == 0 || N == 0 || (A[i] && B[i]), "null A/B");
             XRS_REQUIRE(C[i] != A[i] && C[i] != B[i], "C must not alias A or B");
         }
+        xrs::fence_readers(h);
         xrs::gemm_batched(h, int(count), C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0, false);
     });
 }
@@ -1193,6 +1197,7 @@ extern "C" int xrs_gemm_sym(xrs_handle_t h, double* C, size_t N, double alpha, c
         XRS_REQUIRE(transA ? lda >= N || K == 0 : lda >= K || N == 0, "lda too small");
         XRS_REQUIRE(transB ? ldb >= K || N == 0 : ldb >= N || K == 0, "ldb too small");
         XRS_REQUIRE(C != A && C != B, "C must not alias A or B");
+        xrs::fence_readers(h);
         xrs::gemm_sym(h, C, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
     });
 }

@@ -72,7 +72,9 @@ struct Reader {
         return v;
     }
     std::vector<size_t> get_dims() {
-        std::vector<size_t> v(get<size_t>());
+        const size_t count = get<size_t>();
+        XERUS_REQUIRE(count <= 4096, "Malformed stream: " << count << " dimensions");
+        std::vector<size_t> v(count);
         for (size_t& x : v) x = get<size_t>();
         return v;
     }
@@ -82,8 +84,23 @@ struct Reader {
         Tensor::DimensionTuple dims = get_dims();
         const size_t rep = get<size_t>();
         XERUS_REQUIRE(rep == 1, "Unknown tensor representation " << rep << " in stream (this build reads dense tensors only)");
+        // a malformed size must not wrap: check every product, and (binary) that the payload is in the stream
         size_t n = 1;
-        for (size_t d : dims) n *= d;
+        for (size_t d : dims) {
+            XERUS_REQUIRE(d == 0 || n <= (std::numeric_limits<size_t>::max() / sizeof(value_t)) / d,
+                          "Malformed stream: the tensor size overflows");
+            n *= d;
+        }
+        if (f != FileFormat::TSV) {
+            const std::streampos here = s.tellg();
+            if (here != std::streampos(-1)) {
+                s.seekg(0, std::ios::end);
+                const std::streampos end = s.tellg();
+                s.seekg(here);
+                XERUS_REQUIRE(end != std::streampos(-1) && size_t(end - here) >= n * sizeof(value_t),
+                              "Malformed stream: " << n << " entries announced, fewer in the stream");
+            }
+        }
         std::unique_ptr<value_t[]> data(new value_t[std::max<size_t>(n, 1)]);
         if (f == FileFormat::TSV)
             for (size_t i = 0; i < n; ++i) s >> data[i];

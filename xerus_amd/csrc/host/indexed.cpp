@@ -219,6 +219,8 @@ value_t contract_unconnected(TensorNetwork& _net) {
 
 }  // namespace
 
+std::vector<Index> resolve_indices(const std::vector<Index>& _indices, size_t _degree) { return resolve(_indices, _degree); }
+
 Tensor evaluate_product(const IndexedProduct& _p, const std::vector<Index>& _out) {
     XERUS_REQUIRE(!_p.terms.empty(), "empty product");
     Lowered L = lower(_p);

@@ -225,6 +225,30 @@ void TTTensor::round(const value_t _eps) {
     round(std::vector<size_t>(degree() == 0 ? 0 : degree() - 1, std::numeric_limits<size_t>::max()), _eps);
 }
 
+void TTTensor::soft_threshold(const std::vector<double>& _taus, const bool /*_preventZero*/) {
+    const size_t d = degree();
+    XERUS_REQUIRE(_taus.size() + 1 == d || (_taus.empty() && d == 0),
+                  "There must be exactly degree/N-1 taus. Here " << _taus.size() << " instead of " << d - 1 << " are given.");
+    require_correct_format();
+    if (d == 0) return;
+    const bool initialCanonicalization = canonicalized;
+    const size_t initialCorePosition = corePosition;
+    {
+        Handoff H(*this);
+        guard([&] {
+            xrs::tt::soft_threshold(gpu::handle(), d, H.n.data(), H.r.data(), H.cores.data(), canonicalized, corePosition,
+                                    _taus.data());
+        });
+        H.give_back();
+    }
+    assume_core_position(0);
+    if (initialCanonicalization) move_core(initialCorePosition);
+}
+
+void TTTensor::soft_threshold(const double _tau, const bool _preventZero) {
+    soft_threshold(std::vector<double>(degree() == 0 ? 0 : degree() - 1, _tau), _preventZero);
+}
+
 value_t TTTensor::frob_norm() const {
     require_correct_format();
     if (canonicalized) return components[corePosition].frob_norm();

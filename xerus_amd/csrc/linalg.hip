@@ -427,6 +427,7 @@ extern "C" {
 int xrs_qc(xrs_handle_t h, double* Q, double* C, size_t* rank, const double* A, size_t m, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && Q && C && rank && A, "null argument");
+        fence_readers(h);
         *rank = qc(h, A, m, n, Q, C);
     });
 }
@@ -434,6 +435,7 @@ int xrs_qc(xrs_handle_t h, double* Q, double* C, size_t* rank, const double* A, 
 int xrs_cq(xrs_handle_t h, double* C, double* Q, size_t* rank, const double* A, size_t m, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && Q && C && rank && A, "null argument");
+        fence_readers(h);
         *rank = cq(h, A, m, n, C, Q);
     });
 }
@@ -441,6 +443,7 @@ int xrs_cq(xrs_handle_t h, double* C, double* Q, size_t* rank, const double* A, 
 int xrs_qr(xrs_handle_t h, double* Q, double* R, const double* A, size_t m, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && Q && R && A, "null argument");
+        fence_readers(h);
         qr(h, A, m, n, Q, R);
     });
 }
@@ -448,6 +451,7 @@ int xrs_qr(xrs_handle_t h, double* Q, double* R, const double* A, size_t m, size
 int xrs_rq(xrs_handle_t h, double* R, double* Q, const double* A, size_t m, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && Q && R && A, "null argument");
+        fence_readers(h);
         rq(h, A, m, n, R, Q);
     });
 }
@@ -455,6 +459,7 @@ int xrs_rq(xrs_handle_t h, double* R, double* Q, const double* A, size_t m, size
 int xrs_svd(xrs_handle_t h, double* U, double* S, double* Vt, const double* A, size_t m, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && U && S && Vt && A, "null argument");
+        fence_readers(h);
         svd(h, A, m, n, U, S, Vt);
     });
 }
@@ -462,7 +467,8 @@ int xrs_svd(xrs_handle_t h, double* U, double* S, double* Vt, const double* A, s
 int xrs_svd_rows_vt(xrs_handle_t h, double* S, double* Vt, int* sweeps, const double* A, size_t p, size_t q, int kernel) {
     return guarded([&] {
         XRS_REQUIRE(h && S && Vt && A && sweeps, "null argument");
-        XRS_REQUIRE(p >= 1 && p <= q && q <= 512, "xrs_svd_rows_vt: need 1 <= p <= q <= 512");
+        XRS_REQUIRE(p >= 1 && p <= q && q <= 1024 && (kernel != 1 || p <= 512),
+                    "xrs_svd_rows_vt: need 1 <= p <= q <= 1024 (kernel 1: p <= 512)");
         DevBuf st(h, 64);
         XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
         jacobi_vt(h, A, int(q), false, int(p), int(q), S, Vt, int(q), st.as<int>(), 40, kernel);

@@ -349,6 +349,7 @@ extern "C" int xrs_permute(xrs_handle_t h, double* out, const double* in, size_t
         for (size_t i = 0; i < ndim; ++i) total *= dims[i];
         XRS_REQUIRE(total == 0 || (out && in), "null data pointer");
         XRS_REQUIRE(out != in || total <= 1, "out must not alias in");
+        xrs::fence_readers(h);
         if (ndim == 0) {
             if (total) XRS_HIP(hipMemcpyAsync(out, in, 8, hipMemcpyDeviceToDevice, h->stream));
             return;

@@ -4,6 +4,7 @@
 //     i, j, k = xe.indices(3)
 //     A(i, j) << B(i, k) * C(k, j)
 // Everything computes on the GPU through libxerus_amd; numpy arrays are only the host interchange format.
+#include <limits>
 #include <pybind11/numpy.h>
 #include <pybind11/operators.h>
 #include <pybind11/pybind11.h>
@@ -170,6 +171,34 @@ PYBIND11_MODULE(xerus, m) {
         .def(py::self / value_t())
         .def("__copy__", [](const Tensor& _t) { return Tensor(_t); });
 
+    // factorisation expressions (reference python/factorizations.cpp): (U(i,r), S(r,s), Vt(s,j)) << SVD(A(i,j))
+    py::class_<TensorFactorisation>(m, "TensorFactorisation")
+        .def("__rlshift__", [](const TensorFactorisation& _f, const py::tuple& _lhs) {
+            std::vector<IndexedTensor<Tensor>*> out;
+            for (const auto& o : _lhs) out.push_back(o.cast<IndexedTensor<Tensor>*>());
+            _f(out);
+        });
+    py::class_<SVD, TensorFactorisation>(m, "SVD_temporary");
+    py::class_<QR, TensorFactorisation>(m, "QR_temporary");
+    py::class_<RQ, TensorFactorisation>(m, "RQ_temporary");
+    py::class_<QC, TensorFactorisation>(m, "QC_temporary");
+    py::class_<CQ, TensorFactorisation>(m, "CQ_temporary");
+    // eps defaults to EPSILON, or to 0 with a soft threshold (the C++ SVD(A, softThreshold) constructor)
+    auto def_factorisations = [&m](auto _tag) {
+        using In = decltype(_tag);
+        m.def("SVD", [](const In& _a, size_t _maxRank, py::object _eps, double _soft, bool _preventZero) {
+            const double eps = _eps.is_none() ? (_soft > 0.0 ? 0.0 : EPSILON) : _eps.cast<double>();
+            return new SVD(_a, _maxRank, eps, _soft, _preventZero);
+        }, py::arg("source"), py::arg("maxRank") = std::numeric_limits<size_t>::max(), py::arg("eps") = py::none(),
+              py::arg("softThreshold") = 0.0, py::arg("preventZero") = false, py::keep_alive<0, 1>());
+        m.def("QR", [](const In& _a) { return new QR(_a); }, py::keep_alive<0, 1>());
+        m.def("RQ", [](const In& _a) { return new RQ(_a); }, py::keep_alive<0, 1>());
+        m.def("QC", [](const In& _a) { return new QC(_a); }, py::keep_alive<0, 1>());
+        m.def("CQ", [](const In& _a) { return new CQ(_a); }, py::keep_alive<0, 1>());
+    };
+    def_factorisations(IndexedTensor<Tensor>(nullptr, {}, false));
+    def_factorisations(IndexedProduct());
+
     m.def("contract", py::overload_cast<const Tensor&, bool, const Tensor&, bool, size_t>(&contract));
     m.def("reshuffle", py::overload_cast<const Tensor&, const std::vector<size_t>&>(&reshuffle));
     m.def("frob_norm", [](const Tensor& _t) { return _t.frob_norm(); });
@@ -269,6 +298,10 @@ PYBIND11_MODULE(xerus, m) {
              py::arg("eps") = EPSILON)
         .def("round", py::overload_cast<const size_t>(&TTTensor::round))
         .def("round", py::overload_cast<const value_t>(&TTTensor::round))
+        .def("soft_threshold", py::overload_cast<const std::vector<double>&, const bool>(&TTTensor::soft_threshold), py::arg("taus"),
+             py::arg("preventZero") = false)
+        .def("soft_threshold", py::overload_cast<const double, const bool>(&TTTensor::soft_threshold), py::arg("tau"),
+             py::arg("preventZero") = false)
         .def("frob_norm", &TTTensor::frob_norm)
         .def("exceeds_maximal_ranks", &TTTensor::exceeds_maximal_ranks)
         .def("__call__", [](TTTensor& _t, py::args _a) { return _t(to_indices(_a)); }, py::keep_alive<0, 1>())

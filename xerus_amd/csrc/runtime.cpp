@@ -365,6 +365,7 @@ int xrs_upload(xrs_handle_t h, double* dst, const double* src, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && (n == 0 || (dst && src)), "null argument");
         if (n == 0) return;
+        fence_readers(h);
         XRS_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyHostToDevice, h->stream));
         XRS_HIP(hipStreamSynchronize(h->stream));
     });
@@ -382,6 +383,7 @@ int xrs_download(xrs_handle_t h, double* dst, const double* src, size_t n) {
 int xrs_memset_zero(xrs_handle_t h, double* dst, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && (n == 0 || dst), "null argument");
+        if (n) fence_readers(h);
         if (n) XRS_HIP(hipMemsetAsync(dst, 0, n * sizeof(double), h->stream));
     });
 }
@@ -389,6 +391,7 @@ int xrs_memset_zero(xrs_handle_t h, double* dst, size_t n) {
 int xrs_copy(xrs_handle_t h, double* dst, const double* src, size_t n) {
     return guarded([&] {
         XRS_REQUIRE(h && (n == 0 || (dst && src)), "null argument");
+        if (n) fence_readers(h);
         if (n) XRS_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
     });
 }

@@ -173,8 +173,10 @@ void check_launch(const char* what);
 void host_wait(xrs_handle_t h);
 
 // Order the current stream after an in-flight asynchronous reader of the handle's blocks (the async
-// TT inner product); no-op when none is pending. Called before a block is released and before a TT
-// is mutated in place.
+// TT inner product): a host wait for it (opening its gate first); no-op when none is pending. Called
+// before a block is released and by every C-ABI entry point that writes caller memory (xrs_scal,
+// xrs_axpy, xrs_copy, xrs_upload, xrs_memset_zero, xrs_scale_rows, xrs_gemm*, xrs_permute, the
+// factorisations and solves), so an in-place write to a core never races the product.
 void fence_readers(xrs_handle_t h);
 // blocks until the handle's asynchronous inner product (if any) has finished on the device (tt.hip)
 void wait_dot_done(xrs_handle_t h);

@@ -1312,10 +1312,15 @@ void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, d
         jacobi_usv(h, W, q, false, p, q, U, p, S, Vt, q, st.as<int>(), 60);
         int sweeps = 0;
         read_status(h, st.as<int>(), 1, &sweeps);
-        if (sweeps < 0)
-            std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %d x %d matrix did not converge (status %d)\n",
-                         p, q, sweeps);
-        return;
+        if (sweeps != -2) {
+            if (sweeps < 0)
+                std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %d x %d matrix did not converge (status %d)\n",
+                             p, q, sweeps);
+            return;
+        }
+        // -2: a bounded grid-barrier poll timed out (a workgroup was not scheduled), so the multi-workgroup
+        // result is not valid at all -- not a convergence failure: redo the SVD in one workgroup below
+        std::fprintf(stderr, "[xerus_amd warning] multi-workgroup Jacobi barrier timed out (%d x %d); rerun in one workgroup\n", p, q);
     }
     DevBuf Wc(h, size_t(p) * q * 8), J(h, size_t(p) * p * 8), st(h, 64);
     XRS_HIP(hipMemcpyAsync(Wc.d(), W, size_t(p) * q * 8, hipMemcpyDeviceToDevice, h->stream));

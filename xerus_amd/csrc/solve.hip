@@ -6,7 +6,7 @@
 // The reference's LU (dgesv), LDL^T (dsysv) and dgelsd all return the solution of a nonsingular system
 // (dgelsd: the minimum-norm least-squares solution, singular values <= EPSILON sigma_max dropped); here
 // the general and least-squares paths are one SVD solve x = V S^+ U^T b with that same cut (min(m, n)
-// <= 512), and the Cholesky path is a right-looking blocked factorisation: 256-column diagonal blocks by
+// <= 512; above: a shifted-CholeskyQR3 QR / LQ solve, full rank only), and the Cholesky path is a right-looking blocked factorisation: 256-column diagonal blocks by
 // the register-resident potrf + explicit triangular inverse, panels and trailing updates as MFMA GEMMs
 // (n unbounded). Triangular solves use the diagonal-block inverses, so both sweeps are GEMMs too.
 #include <cmath>
@@ -198,10 +198,63 @@ void chol_solve(xrs_handle_t h, const double* L, const std::vector<DevBuf>& Z, s
     }
 }
 
+// min(m, n) > 512 (no single-workgroup SVD there): shifted CholeskyQR3 (Fukaya et al. 2020) of A with the
+// explicit inverses of its three Cholesky factors, so the triangular solves are GEMMs:
+//   m >= n: A = Q R, R = L3^T L2^T L1^T       -> X = R^{-1} Q^T B = Z1^T Z2^T Z3^T (Q^T B)
+//   m <  n: A = L Q, L = L1 L2 L3             -> X = Q^T L^{-1} B = Q^T Z3 Z2 Z1 B (the minimum-norm solution)
+// Same solution as the reference's dgesv / dgelsd for a matrix of full rank min(m, n) with kappa < 1/u; a
+// numerically rank-deficient system of that size is rejected (XRS_ENUMERIC) instead of getting dgelsd's
+// truncated minimum-norm solution.
+static void qr_solve_big(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p) {
+    const bool wide = m < n;
+    const size_t N = wide ? m : n, M = wide ? n : m;
+    const int nb = chol_full_blocks(N);
+    DevBuf G(h, N * N * 8), Z1(h, N * N * 8), Z2(h, N * N * 8), Z3(h, N * N * 8), Q1(h, m * n * 8), Q2(h, m * n * 8),
+        st(h, size_t(3 * nb) * 4 + 64), Y(h, std::max(M, N) * p * 8), Y2(h, std::max(M, N) * p * 8);
+    XRS_HIP(hipMemsetAsync(st.d(), 0, size_t(3 * nb) * 4, h->stream));
+    auto gram = [&](const double* Xm) {
+        if (wide) gemm_sym(h, G.d(), N, 1.0, Xm, n, false, M, Xm, n, true);   // X X^T
+        else gemm_sym(h, G.d(), N, 1.0, Xm, n, true, M, Xm, n, false);        // X^T X
+    };
+    auto apply = [&](const double* Z, const double* Xm, double* out) {       // tall: X Z^T, wide: Z X
+        if (wide) gemm(h, out, N, n, 1.0, Z, N, false, N, Xm, n, false);
+        else gemm(h, out, m, N, 1.0, Xm, n, false, N, Z, N, true);
+    };
+    const double s_rel = 11.0 * (double(M) * N + double(N) * (N + 1)) * 1.1102230246251565e-16;
+    gram(A);
+    chol_full(h, G.d(), N, s_rel, nullptr, Z1.d(), st.as<int>());
+    apply(Z1.d(), A, Q1.d());
+    gram(Q1.d());
+    chol_full(h, G.d(), N, 0.0, nullptr, Z2.d(), st.as<int>() + nb);
+    apply(Z2.d(), Q1.d(), Q2.d());
+    gram(Q2.d());
+    chol_full(h, G.d(), N, 0.0, nullptr, Z3.d(), st.as<int>() + 2 * nb);
+    double* Q = Q1.d();   // (Q1 no longer needed)
+    apply(Z3.d(), Q2.d(), Q);
+    std::vector<int> sts(size_t(3 * nb));
+    read_status(h, st.as<int>(), 3 * nb, sts.data());
+    for (int v : sts)
+        if (v != 0) throw Error{XRS_ENUMERIC, "solve: a numerically rank-deficient system with min(m, n) > 512 is not supported"};
+    if (!wide) {
+        gemm(h, Y.d(), n, p, 1.0, Q, n, true, m, B, p, false);          // Q^T B
+        gemm(h, Y2.d(), n, p, 1.0, Z3.d(), n, true, n, Y.d(), p, false);  // Z3^T
+        gemm(h, Y.d(), n, p, 1.0, Z2.d(), n, true, n, Y2.d(), p, false);  // Z2^T
+        gemm(h, X, n, p, 1.0, Z1.d(), n, true, n, Y.d(), p, false);       // Z1^T
+    } else {
+        gemm(h, Y.d(), m, p, 1.0, Z1.d(), m, false, m, B, p, false);
+        gemm(h, Y2.d(), m, p, 1.0, Z2.d(), m, false, m, Y.d(), p, false);
+        gemm(h, Y.d(), m, p, 1.0, Z3.d(), m, false, m, Y2.d(), p, false);
+        gemm(h, X, n, p, 1.0, Q, n, true, m, Y.d(), p, false);            // Q^T (L^{-1} B)
+    }
+}
+
 // x = V S^+ U^T b, singular values <= EPSILON sigma_0 dropped (dgelsd with rcond = xerus::EPSILON, :704)
 void svd_solve(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, const double* B, size_t p) {
     const size_t k = std::min(m, n);
-    XRS_REQUIRE(k <= size_t(kSmallMax), "solve: the general / least-squares path needs min(m, n) <= 512");
+    if (k > size_t(kSmallMax)) {
+        qr_solve_big(h, X, A, m, n, B, p);
+        return;
+    }
     DevBuf U(h, m * k * 8), S(h, k * 8), Vt(h, k * n * 8), Si(h, k * 8), T(h, k * p * 8);
     svd(h, A, m, n, U.d(), S.d(), Vt.d());
     hipLaunchKernelGGL(k_inv_cut, dim3(unsigned((k + 255) / 256)), dim3(256), 0, h->stream, S.d(), int(k), 8.0 * kEps, Si.d());
@@ -247,6 +300,7 @@ int xrs_solve(xrs_handle_t h, double* X, const double* A, size_t m, size_t n, co
     return guarded([&] {
         XRS_REQUIRE(h && X && A && B, "null argument");
         XRS_REQUIRE(m > 0 && n > 0 && p > 0, "solve: empty system");
+        fence_readers(h);
         solve_dense(h, X, A, m, n, B, p);
     });
 }
@@ -255,6 +309,7 @@ int xrs_solve_least_squares(xrs_handle_t h, double* X, const double* A, size_t m
     return guarded([&] {
         XRS_REQUIRE(h && X && A && B, "null argument");
         XRS_REQUIRE(m > 0 && n > 0 && p > 0, "solve_least_squares: empty system");
+        fence_readers(h);
         svd_solve(h, X, A, m, n, B, p);
     });
 }

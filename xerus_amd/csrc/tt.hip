@@ -20,6 +20,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <limits>
 #include <mutex>
 #include <thread>
 #include <cstdio>
@@ -124,8 +125,19 @@ size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps) {
     return rank;
 }
 
+// S[i] = max(0, S[i] - soft) for the kept i < kk (round_edge's soft threshold, tensorNetwork.cpp:766, 788)
+__global__ void k_soft_shift(double* __restrict__ S, int kk, double soft) {
+    for (int i = threadIdx.x; i < kk; i += blockDim.x) S[i] = fmax(0.0, S[i] - soft);
+}
+
+static void soft_shift(xrs_handle_t h, double* S, size_t kk, double soft) {
+    if (!(soft > 0.0) || kk == 0) return;
+    hipLaunchKernelGGL(k_soft_shift, dim3(1), dim3(256), 0, h->stream, S, int(kk), soft);
+    check_launch("k_soft_shift");
+}
+
 // truncate the edge between core k-1 and core k (round_edge(k, k-1), core moves to k-1)
-void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
+void truncate_edge(TT& t, size_t k, size_t max_rank, double eps, double soft) {
     const size_t m = t.r[k], nn = t.cols_right(k);
     const size_t prow = t.rows_left(k - 1);
     xrs_handle_t h = t.h;
@@ -133,7 +145,7 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
         double* Q = t.alloc(m * nn);
         double* L = t.alloc(m * m);
         const OrthResult o = orthogonalize(h, t.core[k], m, nn, true, Q, L);
-        if (o.certified && eps < 0.5 * o.cert_ratio && max_rank >= m) {
+        if (o.certified && eps < 0.5 * o.cert_ratio && max_rank >= m && !(soft > 0.0)) {
             double* prv = t.alloc(prow * m);
             gemm(h, prv, prow, m, 1.0, t.core[k - 1], m, false, m, L, m, false);
             t.release(L);
@@ -148,6 +160,7 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
         XRS_HIP(hipMemcpyAsync(s.data(), S.d(), m * 8, hipMemcpyDeviceToHost, h->stream));
         XRS_HIP(hipStreamSynchronize(h->stream));
         const size_t kk = svd_cut(s, max_rank, eps);
+        soft_shift(h, S.d(), kk, soft);
         double* cur = t.alloc(kk * nn);
         gemm(h, cur, kk, nn, 1.0, Vt.d(), m, false, m, Q, nn, false);          // Vt[:kk] Q
         scale_cols(h, U.d(), S.d(), m, m);                                     // U S (columns >= kk unused)
@@ -171,6 +184,7 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps) {
     XRS_HIP(hipMemcpyAsync(s.data(), S.d(), nn * 8, hipMemcpyDeviceToHost, h->stream));
     XRS_HIP(hipStreamSynchronize(h->stream));
     const size_t kk = svd_cut(s, max_rank, eps);
+    soft_shift(h, S.d(), kk, soft);
     double* cur = t.alloc(kk * nn);
     XRS_HIP(hipMemcpyAsync(cur, Vt.d(), kk * nn * 8, hipMemcpyDeviceToDevice, h->stream));
     gemm(h, QU.d(), m, nn, 1.0, Q, nn, false, nn, U.d(), nn, false);
@@ -899,6 +913,16 @@ void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, 
     for (size_t k = d - 1; k >= 1; --k) truncate_edge(t, k, max_ranks[k - 1], eps);
 }
 
+void soft_threshold(TT& t, bool canonicalized, size_t core_pos, const double* taus) {
+    const size_t d = t.d;
+    t.h->last_round_path = XRS_ROUND_REFERENCE;
+    const size_t start = canonicalized ? core_pos : 0;   // canonicalize_right (ttNetwork.cpp:701)
+    for (size_t k = start; k + 1 < d; ++k) orth_right(t, k);
+    // round_edge(numComponents - i, numComponents - i - 1, max, 0.0, taus[i]) (:703-705): edge i counted
+    // from the right end
+    for (size_t i = 0; i + 1 < d; ++i) truncate_edge(t, d - 1 - i, std::numeric_limits<size_t>::max(), 0.0, taus[i]);
+}
+
 // <x, y> with the zipper run from both ends at once (left environments on a side stream, right ones on
 // the main stream) and closed at the middle edge m by sum_ab E_m[a,b] F_m[a,b]: the two chains are
 // independent, so the critical path halves and the two streams fill the chip together.
@@ -1259,6 +1283,12 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
            const double* const* Y) {
     return xrs::dot(h, d, n, rx, X, ry, Y);
 }
+void soft_threshold(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
+                    const double* taus) {
+    check_tt(d, n, r, cores);
+    TT t{h, d, n, r, cores};
+    xrs::soft_threshold(t, canonicalized, core_pos, taus);
+}
 }  // namespace tt
 
 }  // namespace xrs
@@ -1290,6 +1320,18 @@ int xrs_tt_round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** 
         XRS_REQUIRE(!canonicalized || core_position < d, "Illegal current core position");
         TT t{h, d, n, r, cores};
         round(t, canonicalized != 0, core_position, max_ranks, eps);
+    });
+}
+
+int xrs_tt_soft_threshold(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, int canonicalized,
+                          size_t core_position, const double* taus) {
+    return guarded([&] {
+        XRS_REQUIRE(h && (d < 2 || taus), "null argument");
+        check_tt(d, n, r, cores);
+        XRS_REQUIRE(!canonicalized || core_position < d, "Illegal current core position");
+        for (size_t k = 0; k + 1 < d; ++k) XRS_REQUIRE(taus[k] >= 0.0, "soft threshold must not be negative");
+        TT t{h, d, n, r, cores};
+        soft_threshold(t, canonicalized != 0, core_position, taus);
     });
 }
 

@@ -98,7 +98,12 @@ void factor_big(xrs_handle_t h, const std::vector<BigJob>& jobs, int* status, st
 void transfer_right(TT& t, size_t k, bool rank_reduce);   // transfer_core(k -> k+1): QC (or QR) + R * next
 void orth_right(TT& t, size_t k);
 size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps);
-void truncate_edge(TT& t, size_t k, size_t max_rank, double eps);
+// round_edge (tensorNetwork.cpp:678-818) of the edge k-1 | k, core moving to k-1; soft > 0 replaces the
+// kept singular values by max(0, sigma - soft) (round_edge's _softThreshold, :766 / :788)
+void truncate_edge(TT& t, size_t k, size_t max_rank, double eps, double soft = 0.0);
+// TTNetwork::soft_threshold (ttNetwork.cpp:688-713): canonicalize_right, then round_edge(maxRank = inf,
+// eps = 0, soft = taus[i]) over the edges right to left, taus[0] at the last edge (the reference's order)
+void soft_threshold(TT& t, bool canonicalized, size_t core_pos, const double* taus);
 
 // one right chain pass restoring right-orthonormality of nearly orthonormal cores (tt.hip)
 bool reorthonormalize(TT& t);

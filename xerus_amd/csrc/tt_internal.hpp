@@ -11,5 +11,7 @@ void round(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores,
            const size_t* max_ranks, double eps);
 double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
            const double* const* Y);
+void soft_threshold(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
+                    const double* taus);
 }  // namespace tt
 }  // namespace xrs
