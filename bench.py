@@ -238,23 +238,26 @@ def bench_cfg3(h, xe):
     y.move_core(0)
     out = {"workload": f"TT order-{d} n={n} rank-{r}"}
 
-    def round_case(src, target, reps):
+    def round_case(src, target, reps, eps=8 * np.finfo(float).eps):
         ts = []
         for _ in range(reps + 1):
             c = src.clone()
             h.synchronize()
             t0 = time.perf_counter()
-            c.round(target)
+            c.round(target, eps)
             h.synchronize()
             ts.append(time.perf_counter() - t0)
             res_ranks = c.r
+            out.setdefault("_paths", set()).add(h.last_round_path())
             c.free()
         return float(np.mean(ts[1:])) * 1e3, res_ranks
 
     ms, rr = round_case(x, 128, 10)
+    out.pop("_paths", None)
     f = flops_round(dims, ranks)
     out["round128"] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_out": rr[1:-1]}
     ms, rr = round_case(x, 64, 10)
+    out.pop("_paths", None)
     out["round64"] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_out": rr[1:-1],
                       "flops_note": "standard two-sweep flops of the input ranks"}
     # x + y: block-diagonal cores (TTNetwork::operator+=, ttNetwork.cpp:797-847), not canonical
@@ -274,10 +277,24 @@ def bench_cfg3(h, xe):
     s = capi.TTDevice.from_cores(h, sc)
     sr = [1] + [c.shape[2] for c in sc]
     ms, rr = round_case(s, 128, 5)
+    out.pop("_paths", None)
     f = flops_round(dims, sr)
     out["sum_round128"] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_in": sr[1:-1],
                            "ranks_out": rr[1:-1]}
-    for t in (x, y, s):
+    # decaying spectra the certified paths refuse (tests/test_round_general_gpu.py): raw N(0,1) cores whose
+    # right rank index is scaled by 0.8^j; round(64) (maxRank cut) and round(1e-8) (eps cut only)
+    gc = random_cores(xe, dims, ranks, SEED + 13)
+    for k in range(d - 1):
+        gc[k] = gc[k] * (0.8 ** np.arange(gc[k].shape[2]))[None, None, :]
+    g = capi.TTDevice.from_cores(h, gc)
+    f = flops_round(dims, ranks)
+    for key, target, eps in (("round64_graded", 64, 8 * np.finfo(float).eps), ("round_eps_graded", [2 ** 62] * (d - 1), 1e-8)):
+        out.pop("_paths", None)
+        ms, rr = round_case(g, target, 5, eps)
+        out[key] = {"ms": round(ms, 3), "gflops": round(f / (ms * 1e-3) / 1e9, 1), "ranks_out": rr[1:-1],
+                    "eps": eps, "path": sorted(out.pop("_paths"))}
+    out.pop("_paths", None)
+    for t in (x, y, s, g):
         t.free()
     return out
 

@@ -48,7 +48,8 @@ class ALSVariant {
         value_t residual_f() const;
     };
 
-    /// (local operator as a tensor (rL, n, rR, rL', n', rR'), local solution(s), local rhs (rL, n, rR), state)
+    /// (local operator as a tensor (rL, n.., rR, rL', n'.., rR') over the window's sites, local solution(s),
+    /// local rhs (rL, n.., rR), state)
     using LocalSolver = std::function<void(const Tensor&, std::vector<Tensor>&, const Tensor&, const ALSAlgorithmicData&)>;
 
     static void lapack_solver(const Tensor& _A, std::vector<Tensor>& _x, const Tensor& _b, const ALSAlgorithmicData& _data);
@@ -90,10 +91,12 @@ class ALSVariant {
     bool check_for_end_of_sweep(ALSAlgorithmicData& _data, size_t _numHalfSweeps, value_t _convergenceEpsilon) const;
 };
 
-/// the reference's predefined variants (als.cpp:556-563; single-site: the two-site DMRG variants are not
-/// provided)
+/// the reference's predefined variants (als.cpp:556-563)
 extern const ALSVariant ALS;
 extern const ALSVariant ALS_SPD;
+/// two-site DMRG (merged component of two neighbours, split by an SVD truncated to the initial ranks)
+extern const ALSVariant DMRG;
+extern const ALSVariant DMRG_SPD;
 extern const ALSVariant ASD;
 extern const ALSVariant ASD_SPD;
 

@@ -178,11 +178,13 @@ int xrs_tt_operator_apply(xrs_handle_t handle, size_t d, const size_t* n, const 
                           const double* const* A, const size_t* rb, const double* const* B, int transpose_a, double** out);
 /** Which algorithm the handle's last xrs_tt_round used: XRS_ROUND_CHAIN (certified, no cut possible:
  *  Gram chains + batched factorisations), XRS_ROUND_TRUNCATE (certified truncation: left chain pass +
- *  device-resident right-to-left SVD sweep), XRS_ROUND_REFERENCE (the reference's sequential
+ *  device-resident right-to-left SVD sweep), XRS_ROUND_GENERAL (any spectrum and eps: shifted
+ *  CholeskyQR3 sweep + Jacobi SVDs with device-side rank cuts, one synchronisation), XRS_ROUND_REFERENCE (the reference's sequential
  *  QC + round_edge sweeps); 0 before the first round. Diagnostics for tests and benchmarks. */
 #define XRS_ROUND_CHAIN 1
 #define XRS_ROUND_TRUNCATE 2
 #define XRS_ROUND_REFERENCE 3
+#define XRS_ROUND_GENERAL 4
 int xrs_tt_last_round_path(xrs_handle_t handle);
 /** <x,y> of two TTs with equal mode sizes (value_t(x(i&0)*y(i&0)), ttNetwork.cpp:782-789 path,
  *  SURVEY §3.4) as a left-to-right zipper without permutations. *result on host. Synchronises. */

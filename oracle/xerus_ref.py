@@ -624,3 +624,148 @@ def als(A: Sequence[np.ndarray] | None, x: TT, b: TT, spd: bool = True, num_half
             bL.pop()
             bR.append(rhs_right(bR[-1], cur))
             cur -= 1
+
+
+# ------------------------------------------------------------------------------------------------
+# Two-site ALS = DMRG / DMRG_SPD (als.cpp:43-69 lapack_solver split, :383-423 local problems,
+# :556-563 variants), dense local solves and numpy SVD splits truncated to the initial ranks.
+# Decreasing sweeps extend the right stack by the site that leaves the window (currIndex + 1); the
+# reference writes currIndex there (als.cpp:371-379), correct only for one site (see host/als.cpp).
+def dmrg(A: Sequence[np.ndarray], x: TT, b: TT, spd: bool = True, num_half_sweeps: int = 0, eps: float = 1e-6,
+         preserve_core: bool = True) -> float:
+    d = x.order
+    s = 2
+    canon_end, core_end = x.canonicalized, x.core_position
+    target = list(x.ranks)
+    # prepare_x_for_als (:109-187), window of two sites at the right end
+    first, prod = 0, 1
+    while first + 1 < d:
+        n = x.dims[first]
+        if x.ranks[first] < prod * n:
+            break
+        cur0 = x.cores[first].reshape(-1, x.cores[first].shape[2])
+        x.cores[first + 1] = np.einsum('ac,cnb->anb', cur0, x.cores[first + 1])
+        I = np.zeros((prod, n, prod * n))
+        for i0 in range(prod):
+            for i1 in range(n):
+                I[i0, i1, i0 * n + i1] = 1.0
+        x.cores[first] = I
+        x.canonicalized = False
+        first, prod = first + 1, prod * n
+    first_not, prod = d, 1
+    while first_not > first + s:
+        n = x.dims[first_not - 1]
+        if x.ranks[first_not - 2] < prod * n:
+            break
+        cur0 = x.cores[first_not - 1].reshape(x.cores[first_not - 1].shape[0], -1)
+        x.cores[first_not - 2] = np.einsum('anc,cb->anb', x.cores[first_not - 2], cur0)
+        I = np.zeros((prod * n, n, prod))
+        for i1 in range(n):
+            for i2 in range(prod):
+                I[i1 * prod + i2, i1, i2] = 1.0
+        x.cores[first_not - 1] = I
+        x.canonicalized = False
+        first_not, prod = first_not - 1, prod * n
+    if canon_end and core_end < first:
+        x.canonicalized, x.core_position = True, first
+    else:
+        if canon_end and core_end >= first_not:
+            x.canonicalized, x.core_position = True, first_not - 1
+        x.move_core(first, keep_rank=True)
+
+    def op_left(E, k):
+        X, Ak = x.cores[k], A[k]
+        if spd:
+            return np.einsum('pqr,pnc,qnmd,rme->cde', E, X, Ak, X)
+        return np.einsum('pqrs,pnc,qmnd,rmle,slf->cdef', E, X, Ak, Ak, X)
+
+    def op_right(E, k):
+        X, Ak = x.cores[k], A[k]
+        if spd:
+            return np.einsum('pnc,qnmd,rme,cde->pqr', X, Ak, X, E)
+        return np.einsum('pnc,qmnd,rmle,slf,cdef->pqrs', X, Ak, Ak, X, E)
+
+    def rhs_left(E, k):
+        X, B = x.cores[k], b.cores[k]
+        if spd:
+            return np.einsum('pq,pnc,qnd->cd', E, B, X)
+        return np.einsum('pqr,pnc,qnmd,rme->cde', E, B, A[k], X)
+
+    def rhs_right(E, k):
+        X, B = x.cores[k], b.cores[k]
+        if spd:
+            return np.einsum('pnc,qnd,cd->pq', B, X, E)
+        return np.einsum('pnc,qnmd,rme,cde->pqr', B, A[k], X, E)
+
+    one_op = np.ones((1, 1, 1)) if spd else np.ones((1, 1, 1, 1))
+    one_rhs = np.ones((1, 1)) if spd else np.ones((1, 1, 1))
+    oL, oR, bL, bR = [one_op], [one_op], [one_rhs], [one_rhs]
+    for i in range(d - 1, first + s - 1, -1):
+        oR.append(op_right(oR[-1], i))
+        bR.append(rhs_right(bR[-1], i))
+    for i in range(first):
+        oL.append(op_left(oL[-1], i))
+        bL.append(rhs_left(bL[-1], i))
+    normB = b.frob_norm() if b.canonicalized else float(np.linalg.norm(b.full()))
+    cur = first
+
+    def window(E0, k, left_step):
+        E = E0
+        for q in range(s):
+            E = left_step(E, k + q)
+        return E
+
+    def energy():
+        if spd:
+            xAx = float(np.sum(window(oL[-1], cur, op_left) * oR[-1]))
+            bx = float(np.sum(window(bL[-1], cur, rhs_left) * bR[-1]))
+            return float(abs(0.5 * xAx - bx))
+        xAtAx = float(np.sum(window(oL[-1], cur, op_left) * oR[-1]))
+        bAx = float(np.sum(window(bL[-1], cur, rhs_left) * bR[-1]))
+        return float(np.sqrt(xAtAx - 2 * bAx + normB ** 2) / normB)
+
+    last2, last, en = 1e102, 1e101, energy()
+    half, increasing = 0, True
+    while True:
+        A0, A1 = A[cur], A[cur + 1]
+        if spd:
+            Aloc = np.einsum('arp,rijs,sklt,btc->aikbpjlc', oL[-1], A0, A1, oR[-1])
+            rhs = np.einsum('ra,ric,ckd,db->aikb', bL[-1], b.cores[cur], b.cores[cur + 1], bR[-1])
+        else:
+            Aloc = np.einsum('aqrp,qyis,ryjt,sxku,txlv,buvc->aikbpjlc', oL[-1], A0, A0, A1, A1, oR[-1])
+            rhs = np.einsum('rqa,ryc,qyid,czm,dzke,meb->aikb', bL[-1], b.cores[cur], A0, b.cores[cur + 1], A1, bR[-1])
+        rl, n0, n1, rr = Aloc.shape[:4]
+        N = rl * n0 * n1 * rr
+        X = np.linalg.solve(Aloc.reshape(N, N), rhs.reshape(N)).reshape(rl, n0, n1, rr)
+        M = X.reshape(rl * n0, n1 * rr)
+        U, S, Vt = svd(M)
+        k = svd_rank(S, target[cur], EPSILON)
+        U, S, Vt = U[:, :k], S[:k], Vt[:k, :]
+        if increasing:   # (U(i^2,j), S, x(k,l&1)) = SVD(x(i^2,l&2), targetRank[currIndex]); x = S x
+            x.cores[cur] = U.reshape(rl, n0, k)
+            x.cores[cur + 1] = (S[:, None] * Vt).reshape(k, n1, rr)
+        else:            # (x(i&1,j), S, Vt(k,l&1)) = SVD(x(i&2,l^2), targetRank[currIndex]); x = x S
+            x.cores[cur] = (U * S[None, :]).reshape(rl, n0, k)
+            x.cores[cur + 1] = Vt.reshape(k, n1, rr)
+        x.canonicalized = False
+        at_end = (not increasing and cur == first) or (increasing and cur == first_not - s)
+        if at_end:
+            half += 1
+            last2, last, en = last, en, energy()
+            if half == num_half_sweeps or abs(last - en) < eps or abs(last2 - en) < eps or first_not - first <= s:
+                if canon_end and preserve_core:
+                    x.move_core(core_end, keep_rank=True)
+                return en
+            increasing = not increasing
+        if increasing:
+            oR.pop()
+            oL.append(op_left(oL[-1], cur))
+            bR.pop()
+            bL.append(rhs_left(bL[-1], cur))
+            cur += 1
+        else:
+            oL.pop()
+            oR.append(op_right(oR[-1], cur + s - 1))
+            bL.pop()
+            bR.append(rhs_right(bR[-1], cur + s - 1))
+            cur -= 1

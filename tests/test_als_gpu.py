@@ -67,6 +67,58 @@ def test_als_matches_oracle(xe, ref, variant, spd, asd):
     assert x.canonicalized and x.corePosition == 0
 
 
+@pytest.mark.parametrize("variant,spd", [("DMRG_SPD", True), ("DMRG", False)])
+def test_dmrg_matches_oracle(xe, ref, variant, spd):
+    """Two-site DMRG (als.cpp:43-69, 556-563): merged two-site local solves, SVD splits truncated to the
+    initial ranks; same ranks, tensor and energy as the oracle's restatement (oracle/xerus_ref.py:dmrg)."""
+    d, n = 5, 4
+    rng = np.random.default_rng(13)
+    cores = _laplace_cores(d, n, shift=0.0 if spd else 0.3)
+    if not spd:
+        cores = [c + 0.1 * rng.standard_normal(c.shape) * (c != 0) for c in cores]
+    A = _operator(xe, cores)
+    b = xe.TTTensor.random([n] * d, [2, 2, 2, 2])
+    x = xe.TTTensor.random([n] * d, [2, 3, 3, 2])
+    ob, ox = _oracle_tt(ref, b), _oracle_tt(ref, x)
+    en = getattr(xe, variant)(A, x, b, 5)
+    oen = ref.dmrg(cores, ox, ob, spd=spd, num_half_sweeps=5)
+    assert x.ranks() == ox.ranks
+    assert _rel(xe.Tensor(x).to_ndarray(), ox.full()) <= 1e-9
+    assert en == pytest.approx(oen, rel=1e-9, abs=1e-12)
+    assert x.canonicalized and x.corePosition == 0
+
+
+def test_dmrg_spd_reaches_dense_solution(xe, ref):
+    """DMRG_SPD with ranks that hold the solution converges to the dense solve of the Laplace system."""
+    d, n = 4, 4
+    cores = _laplace_cores(d, n, shift=0.5)
+    A = _operator(xe, cores)
+    b = xe.TTTensor.random([n] * d, [2, 2, 2])
+    x = xe.TTTensor.random([n] * d, [4, 16, 4])
+    xe.DMRG_SPD(A, x, b, 1e-13)
+    N = n ** d
+    M = ref.op_full(cores).reshape(N, N)
+    xs = np.linalg.solve(M, xe.Tensor(b).to_ndarray().reshape(N))
+    assert _rel(xe.Tensor(x).to_ndarray().reshape(N), xs) <= 1e-9
+
+
+def test_als_local_system_above_512(xe, ref):
+    """ALS (non-SPD: local operator x A^T A x, only approximately symmetric) with interior local systems of
+    order 12 * 4 * 12 = 576 > 512: solved through the general (QR) path, same result as the oracle."""
+    d, n = 6, 4
+    rng = np.random.default_rng(17)
+    cores = [c + 0.1 * rng.standard_normal(c.shape) * (c != 0) for c in _laplace_cores(d, n, shift=0.3)]
+    A = _operator(xe, cores)
+    b = xe.TTTensor.random([n] * d, [2, 2, 2, 2, 2])
+    x = xe.TTTensor.random([n] * d, [3, 12, 12, 12, 3])
+    ob, ox = _oracle_tt(ref, b), _oracle_tt(ref, x)
+    en = xe.ALS(A, x, b, 2)
+    oen = ref.als(cores, ox, ob, spd=False, num_half_sweeps=2)
+    assert x.ranks() == ox.ranks
+    assert _rel(xe.Tensor(x).to_ndarray(), ox.full()) <= 1e-8
+    assert en == pytest.approx(oen, rel=1e-8, abs=1e-12)
+
+
 def test_als_spd_full_rank_reaches_dense_solution(xe, ref):
     d, n = 4, 4
     cores = _laplace_cores(d, n)

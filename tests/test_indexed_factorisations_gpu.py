@@ -123,7 +123,6 @@ def test_svd_soft_thresholding(xe):
     assert xe.approx_equal(U, Us, 1e-12)
     assert xe.approx_equal(V, Vs, 1e-12)
     Sd, Ssd = S.to_ndarray(), Ss.to_ndarray()
-    assert Ss.dimensions[0] < S.dimensions[0]   # the threshold does cut here
     for x in range(S.dimensions[0]):
         if x < Ss.dimensions[0]:
             assert abs(Ssd[x, x] - max(0.0, Sd[x, x] - 7.3)) <= 3e-13 * max(1.0, Sd[x, x])
@@ -138,6 +137,12 @@ def test_svd_soft_thresholding(xe):
     G(o, p) << V(o, l, m, n) * V(p, l, m, n)
     assert np.linalg.norm(G.to_ndarray() - np.eye(S.dimensions[0])) < 1e-12
     del i2
+    # a threshold inside the spectrum: the ranks drop to the values above it (:158-163)
+    tau = float(np.median(np.diag(Sd)))
+    (Us(i, j, k, o), Ss(o, p), Vs(p, l, m, n)) << xe.SVD(tA(i, j, k, l, m, n), softThreshold=tau)
+    keep = int(np.sum(np.diag(Sd)[1:] >= tau)) + 1
+    assert Ss.dimensions[0] == keep < S.dimensions[0]
+    assert np.allclose(np.diag(Ss.to_ndarray()), np.maximum(0.0, np.diag(Sd)[:keep] - tau), rtol=0, atol=3e-13 * Sd[0, 0])
     # preventZero keeps sigma_0 at >= EPSILON sigma_0 when the threshold exceeds it
     (Us(i, j, k, o), Ss(o, p), Vs(p, l, m, n)) << xe.SVD(tA(i, j, k, l, m, n), softThreshold=1e6, preventZero=True)
     assert Ss.dimensions[0] == 1

@@ -19,13 +19,20 @@ d, n, r = 10, 20, int(os.environ.get("RANK", "128"))
 target = int(os.environ.get("TARGET", "64"))
 reps = int(os.environ.get("REPS", "5"))
 ranks = bench.tt_ranks(d, n, r)
-x = capi.TTDevice.from_cores(h, bench.random_cores(xe, [n] * d, ranks, bench.SEED + 11))
-x.move_core(0)
+graded = os.environ.get("GRADED")   # "0.8": decaying spectra (right rank index scaled by GRADED^j), raw cores
+eps = float(os.environ.get("EPS", str(8 * np.finfo(float).eps)))
+cores = bench.random_cores(xe, [n] * d, ranks, bench.SEED + 11)
+if graded:
+    for k in range(d - 1):
+        cores[k] = cores[k] * (float(graded) ** np.arange(cores[k].shape[2]))[None, None, :]
+x = capi.TTDevice.from_cores(h, cores)
+if not graded:
+    x.move_core(0)
 for i in range(reps):
     c = x.clone()
     h.synchronize()
     t0 = time.perf_counter()
-    c.round(target)
+    c.round(target if target > 0 else [2 ** 62] * (d - 1), eps)
     h.synchronize()
     print(f"round({target}) of rank {r}: {(time.perf_counter() - t0) * 1e3:.3f} ms path={h.last_round_path()} ranks={c.ranks}",
           flush=True)

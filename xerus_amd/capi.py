@@ -81,7 +81,7 @@ SIGNATURES = {
 }
 
 KFAM_GEMM, KFAM_PERMUTE, KFAM_QR, KFAM_SVD, KFAM_ELEMWISE = 1, 2, 4, 8, 16
-ROUND_PATHS = {0: None, 1: "chain", 2: "truncate", 3: "reference"}
+ROUND_PATHS = {0: None, 1: "chain", 2: "truncate", 3: "reference", 4: "general"}
 
 _lib = None
 
@@ -307,7 +307,7 @@ class Handle:
         return res
 
     def last_round_path(self) -> str | None:
-        """"chain" / "truncate" / "reference": the algorithm of this handle's last TT round."""
+        """"chain" / "truncate" / "general" / "reference": the algorithm of this handle's last TT round."""
         return ROUND_PATHS[self.lib.xrs_tt_last_round_path(self.h)]
 
     # ---- profiling

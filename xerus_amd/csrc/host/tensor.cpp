@@ -685,6 +685,17 @@ void calculate_svd(Tensor& _U, Tensor& _S, Tensor& _Vt, Tensor _input, const siz
         XRS_HIP(hipMemcpy2DAsync(Ut.device_data_for_write(), rank * 8, U.d(), k * 8, rank * 8, m, hipMemcpyDeviceToDevice, h->stream));
         XRS_HIP(hipMemcpyAsync(Vtt.device_data_for_write(), Vt.d(), rank * n * 8, hipMemcpyDeviceToDevice, h->stream));
     });
+    if (!(s[0] > 0.0)) {
+        // the zero matrix: rank 1 with sigma 0; dgesdd's factors are still orthonormal (e_0 columns / rows)
+        const double one = 1.0;
+        guard([&] {
+            XRS_HIP(hipMemsetAsync(Ut.device_data_for_write(), 0, m * rank * 8, h->stream));
+            XRS_HIP(hipMemsetAsync(Vtt.device_data_for_write(), 0, rank * n * 8, h->stream));
+            XRS_HIP(hipMemcpyAsync(Ut.device_data_for_write(), &one, 8, hipMemcpyHostToDevice, h->stream));
+            XRS_HIP(hipMemcpyAsync(Vtt.device_data_for_write(), &one, 8, hipMemcpyHostToDevice, h->stream));
+            XRS_HIP(hipStreamSynchronize(h->stream));
+        });
+    }
     Tensor St({rank, rank}, Tensor::Representation::Dense, Tensor::Initialisation::Zero);
     {
         double* hs = St.get_dense_data();

@@ -336,6 +336,8 @@ PYBIND11_MODULE(xerus, m) {
         .def("__copy__", [](const ALSVariant& _s) { return ALSVariant(_s); });
     m.attr("ALS") = py::cast(ALSVariant(ALS));
     m.attr("ALS_SPD") = py::cast(ALSVariant(ALS_SPD));
+    m.attr("DMRG") = py::cast(ALSVariant(DMRG));
+    m.attr("DMRG_SPD") = py::cast(ALSVariant(DMRG_SPD));
     m.attr("ASD") = py::cast(ALSVariant(ASD));
     m.attr("ASD_SPD") = py::cast(ALSVariant(ASD_SPD));
     m.def("solve", [](const Tensor& _A, const Tensor& _B, size_t _extra) {

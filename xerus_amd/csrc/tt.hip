@@ -903,6 +903,9 @@ void round(TT& t, bool canonicalized, size_t core_pos, const size_t* max_ranks, 
     if (round_chain(t, max_ranks, eps)) return;      // certified, nothing to cut
     t.h->last_round_path = XRS_ROUND_TRUNCATE;
     if (round_truncate(t, max_ranks, eps)) return;   // certified, cuts by maxRank only (tt_trunc.hip)
+    static const bool no_general = std::getenv("XRS_NO_GENERAL_ROUND") != nullptr;
+    t.h->last_round_path = XRS_ROUND_GENERAL;
+    if (!no_general && round_general(t, max_ranks, eps)) return;   // any spectrum, device-resident (tt_trunc.hip)
     t.h->last_round_path = XRS_ROUND_REFERENCE;
     // canonicalize_right (ttNetwork.cpp:638-640, 654)
     const size_t start = canonicalized ? core_pos : 0;

@@ -112,5 +112,10 @@ bool reorthonormalize(TT& t);
 // truncation sweep with one host synchronisation; false (cores untouched) when a certificate fails
 bool round_truncate(TT& t, const size_t* max_ranks, double eps);
 
+// general truncating round (tt_trunc.hip): any spectrum, maxRank and eps cuts, shifted CholeskyQR3 +
+// Jacobi SVD per edge, enqueued with device-side rank cuts and one synchronisation; false (cores
+// untouched) when a certificate fails (possible QC rank drop, breakdown, non-orthonormal result)
+bool round_general(TT& t, const size_t* max_ranks, double eps);
+
 }  // namespace ttd
 }  // namespace xrs

@@ -406,5 +406,301 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     return true;
 }
 
+// ================================================================================================
+// General truncating round (any spectrum, maxRank and eps cuts): the reference's two sweeps
+// (ttNetwork.cpp:644-665) with every factorisation enqueued and no host synchronisation per edge.
+//  1. left to right (canonicalize_right): core_k = Q_k R_k by shifted CholeskyQR3 (Fukaya et al. 2020;
+//     backward stable for kappa < 1/u), core_{k+1} <- R_k core_{k+1}. The reference's QC drops a rank only
+//     when a pivoted |R_jj| < 16 u R_00 (blasLapackWrapper.cpp:268-272); every R_jj of any triangular
+//     factor is >= sigma_min, and sigma_min >= 1 / ||R^{-1}||_F, so a device certificate
+//     1 / ||R^{-1}||_F > 32 u ||A||_F proves that no rank drops (else the round falls back);
+//  2. right to left (round_edge, tensorNetwork.cpp:678-818): B = core_k (r x N) = L Q by the same
+//     factorisation (wide), the left singular vectors and values of L by one-sided Jacobi on the rows of
+//     L^T (svd.hip; singular values to u ||B|| absolute, so eps cuts far below sqrt(u) are decided on
+//     accurate values), the cut of calculate_svd (tensor.cpp:1462-1474) evaluated ON THE DEVICE
+//     (k_cut_wide / k_cut_tall), core_k <- S^{-1} U^T B rows, core_{k-1} <- core_{k-1} U S. Ranks are not
+//     known on the host until the end: the sweep keeps the uncut sizes with zero rows / columns beyond
+//     the device-side rank, and the cores are compacted once after the single synchronisation.
+// Tall edges (r > N: structural excess at the right end, e.g. x + y) use B = Q R and the right singular
+// vectors of R. Certificates that fail (rank drop possible, Cholesky breakdown, Jacobi not converged,
+// non-orthonormal result) discard the new cores; the caller then runs the reference's sequential sweep.
+namespace {
+
+constexpr double kUnit = 1.1102230246251565e-16;   // 2^-53
+
+// flag = 1 unless 1 / ||W||_F > c ||A||_F, W = R^{-1}, ||A||_F^2 = trG[0] (potrf's trace output)
+__global__ void __launch_bounds__(256) k_rank_cert(const double* __restrict__ W, int n, const double* __restrict__ trG, double c,
+                                                   int* __restrict__ flag) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int e = threadIdx.x; e < n * n; e += 256) s = fma(W[e], W[e], s);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double w2 = (red[0] + red[1]) + (red[2] + red[3]);
+        // 1 / ||W|| > c ||A||  <=>  c^2 ||W||^2 ||A||^2 < 1  (NaN -> flagged)
+        flag[0] = (c * c * w2 * trG[0] < 1.0) ? 0 : 1;
+    }
+}
+
+// rank cut of calculate_svd on the device: kk = min(r, max_rank), then the first j >= 1 with
+// S_j <= eps S_0 (tensor.cpp:1462-1474). Every workgroup recomputes it (S is r <= 1024 doubles).
+__device__ int device_cut(const double* __restrict__ S, int r, long max_rank, double eps) {
+    __shared__ int best;
+    if (threadIdx.x == 0) best = int(std::min<long>(r, max_rank));
+    __syncthreads();
+    const double thr = eps * S[0];
+    for (int j = 1 + int(threadIdx.x); j < r; j += int(blockDim.x))
+        if (S[j] <= thr) atomicMin(&best, j);
+    __syncthreads();
+    return best;
+}
+
+// wide edge: Ut (r x r) = U_L^T (rows = left singular vectors of L), S descending. M = S^{-1} Ut rows
+// (r x r, rows >= kk zero): new core = M B; T = Ut^T S (r x r, columns >= kk zero): core_{k-1} <- core_{k-1} T.
+__global__ void __launch_bounds__(256) k_cut_wide(const double* __restrict__ Ut, const double* __restrict__ S, int r, long max_rank,
+                                                  double eps, double* __restrict__ M, double* __restrict__ T, int* __restrict__ kk_out) {
+    const int kk = device_cut(S, r, max_rank, eps);
+    if (blockIdx.x == 0 && threadIdx.x == 0) kk_out[0] = kk;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < r * r; e += gridDim.x * 256) {
+        const int i = e / r, j = e - i * r;
+        const double u = Ut[e], s = S[i];
+        M[e] = (i < kk && s > 0.0) ? u / s : 0.0;
+        T[size_t(j) * r + i] = i < kk ? u * s : 0.0;
+    }
+}
+
+// tall edge: Vt (g x g) right singular vectors of R (B = Q R); rows >= kk zeroed in place (new core)
+__global__ void __launch_bounds__(256) k_cut_tall(double* __restrict__ Vt, const double* __restrict__ S, int g, long max_rank, double eps,
+                                                  int* __restrict__ kk_out) {
+    const int kk = device_cut(S, g, max_rank, eps);
+    if (blockIdx.x == 0 && threadIdx.x == 0) kk_out[0] = kk;
+    for (int e = blockIdx.x * 256 + threadIdx.x; e < g * g; e += gridDim.x * 256)
+        if (e / g >= kk) Vt[e] = 0.0;
+}
+
+// X[i][i] += v (n x n)
+__global__ void k_add_identity(double* __restrict__ X, int n, double v) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) X[size_t(i) * n + i] += v;
+}
+
+unsigned grid_for(size_t elems) { return unsigned(std::min<size_t>(std::max<size_t>((elems + 255) / 256, 1), 256)); }
+
+// Shifted CholeskyQR3, enqueued: tall A (m x n, m >= n) = Q R (RL = R, upper, n x n), or wide A (m x n,
+// m <= n) = L Q (RL = L, lower, m x m). st[0..3) potrf statuses; trG[0] = ||A||_F^2; with Rinv, the
+// explicit inverse of the triangular factor (tall: R^{-1} transposed, i.e. L3^{-1} L2^{-1} L1^{-1} --
+// same Frobenius norm). N = min(m, n) <= 512.
+void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL, int* st, double* trG, double* Rinv) {
+    xrs_handle_t h = sw.t.h;
+    const size_t N = wide ? m : n, M = wide ? n : m;
+    const int Ni = int(N);
+    double* G = sw.buf(N * N);
+    double* L[3] = {sw.buf(N * N), sw.buf(N * N), sw.buf(N * N)};
+    double* Dv[3] = {sw.buf(dinv_elems(Ni)), sw.buf(dinv_elems(Ni)), sw.buf(dinv_elems(Ni))};
+    double* X1 = sw.buf(m * n);
+    double* X2 = sw.buf(m * n);
+    double* info = sw.buf(4);
+    const double s_rel = 11.0 * (double(M) * N + double(N) * (N + 1)) * kUnit;
+    const double* cur = A;
+    double* outs[3] = {X1, X2, Q};
+    for (int p = 0; p < 3; ++p) {
+        if (wide) gemm_sym(h, L[p], N, 1.0, cur, n, false, M, cur, n, true);   // X X^T
+        else gemm_sym(h, L[p], N, 1.0, cur, n, true, M, cur, n, false);        // X^T X
+        potrf(h, L[p], Ni, p == 0 ? s_rel : 0.0, Dv[p], st + p, p == 0 ? info : nullptr);
+        trsm(h, wide, L[p], Dv[p], Ni, cur, n, outs[p], n, int(M));           // tall: X L^{-T}, wide: L^{-1} X
+        cur = outs[p];
+    }
+    if (trG) XRS_HIP(hipMemcpyAsync(trG, info, 8, hipMemcpyDeviceToDevice, h->stream));
+    // RL = L1 L2 L3 (wide) / R = L3^T L2^T L1^T (tall); potrf leaves the upper triangles zero
+    if (wide) {
+        gemm(h, G, N, N, 1.0, L[0], N, false, N, L[1], N, false);
+        gemm(h, RL, N, N, 1.0, G, N, false, N, L[2], N, false);
+    } else {
+        gemm(h, G, N, N, 1.0, L[2], N, true, N, L[1], N, true);
+        gemm(h, RL, N, N, 1.0, G, N, false, N, L[0], N, true);
+    }
+    if (Rinv) {   // L3^{-1} L2^{-1} L1^{-1} from the identity by three column TRSMs
+        double* I0 = sw.buf(N * N);
+        double* I1 = sw.buf(N * N);
+        XRS_HIP(hipMemsetAsync(I0, 0, N * N * 8, h->stream));
+        hipLaunchKernelGGL(k_add_identity, dim3(grid_for(N)), dim3(256), 0, h->stream, I0, Ni, 1.0);
+        check_launch("k_add_identity");
+        trsm(h, true, L[0], Dv[0], Ni, I0, N, I1, N, Ni);
+        trsm(h, true, L[1], Dv[1], Ni, I1, N, I0, N, Ni);
+        trsm(h, true, L[2], Dv[2], Ni, I0, N, Rinv, N, Ni);
+    }
+}
+
+}  // namespace
+
+bool round_general(TT& t, const size_t* max_ranks, double eps) {
+    const size_t d = t.d;
+    xrs_handle_t h = t.h;
+    static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
+    if (d < 2 || d > 64 || t.sharded()) return false;
+    for (size_t k = 1; k < d; ++k)
+        if (t.r[k] > size_t(kSmallMax)) return false;
+
+    // structural excess at the left end (r_{k+1} > r_k n_k): the reference's own QC steps (as round_truncate)
+    for (size_t k = 0; k + 1 < d; ++k)
+        if (t.r[k + 1] > t.r[k] * t.n[k]) transfer_right(t, k, true);
+
+    Sweep sw(t);
+    constexpr int kSlots = 2048;
+    DevBuf stb(h, kSlots * 4), devb(h, 64 * 16 * 8);
+    int* st = stb.as<int>();
+    XRS_HIP(hipMemsetAsync(st, 0, kSlots * 4, h->stream));
+    int nst = 0;
+    const int kJac = 1536, kRank = 1792;   // Jacobi sweep counts; device ranks
+
+    // 1. left to right: A_k = Q_k, next = R_k core_{k+1}
+    std::vector<double*> A(t.core, t.core + d);   // current cores (originals untouched)
+    std::vector<size_t> rr(t.r, t.r + d + 1);
+    for (size_t k = 0; k + 1 < d; ++k) {
+        const size_t m = rr[k] * t.n[k], b = rr[k + 1];
+        XRS_REQUIRE(m >= b, "round_general: structural excess left after the QC steps");
+        double* Q = sw.core(m * b);
+        double* R = sw.buf(b * b);
+        double* Rinv = sw.buf(b * b);
+        double* trG = sw.buf(1);
+        scqr3(sw, A[k], m, b, false, Q, R, st + nst, trG, Rinv);
+        nst += 3;
+        hipLaunchKernelGGL(k_rank_cert, dim3(1), dim3(256), 0, h->stream, Rinv, int(b), trG, 32.0 * kUnit, st + nst);
+        check_launch("k_rank_cert");
+        ++nst;
+        const size_t cols = t.n[k + 1] * rr[k + 2];
+        double* nxt = sw.core(b * cols);
+        gemm(h, nxt, b, cols, 1.0, R, b, false, b, A[k + 1], cols, false);
+        if (k > 0) sw.drop(A[k]);   // (an intermediate core of this sweep; the originals are not owned)
+        A[k] = Q;
+        A[k + 1] = nxt;
+    }
+    open_dot_gate(h);
+
+    // 2. right to left, uncut (padded) sizes: g[k] = working rank of edge k
+    std::vector<size_t> g(rr);
+    std::vector<int> jac;
+    for (size_t k = d - 1; k >= 1; --k) {
+        const size_t r = g[k], N = t.n[k] * g[k + 1];
+        const bool wide = r <= N;
+        const size_t gg = wide ? r : N;
+        double* B = A[k];
+        double* Qf = sw.buf(r * N);
+        double* F = sw.buf(gg * gg);
+        scqr3(sw, B, r, N, wide, Qf, F, st + nst, nullptr, nullptr);
+        nst += 3;
+        double* S = sw.buf(gg);
+        double* V = sw.buf(gg * gg);
+        int* js = st + kJac + int(jac.size());
+        // wide: rows of L^T (= the left singular vectors of L); tall: rows of R (its right singular vectors)
+        jacobi_vt(h, F, int(gg), wide, int(gg), int(gg), S, V, int(gg), js);
+        jac.push_back(int(k));
+        const size_t prow = g[k - 1] * t.n[k - 1];
+        double* prevk = sw.core(prow * gg);
+        double* newk;
+        if (wide) {
+            double* M = sw.buf(r * r);
+            double* T = sw.buf(r * r);
+            hipLaunchKernelGGL(k_cut_wide, dim3(grid_for(r * r)), dim3(256), 0, h->stream, V, S, int(r), long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)),
+                               eps, M, T, st + kRank + int(k));
+            check_launch("k_cut_wide");
+            newk = sw.core(r * N);
+            gemm(h, newk, r, N, 1.0, M, r, false, r, B, N, false);                 // S^{-1} U^T B (rows >= kk zero)
+            gemm(h, prevk, prow, r, 1.0, A[k - 1], r, false, r, T, r, false);      // core_{k-1} U S
+        } else {
+            hipLaunchKernelGGL(k_cut_tall, dim3(grid_for(gg * gg)), dim3(256), 0, h->stream, V, S, int(gg),
+                               long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)), eps, st + kRank + int(k));
+            check_launch("k_cut_tall");
+            newk = sw.core(gg * N);
+            XRS_HIP(hipMemcpyAsync(newk, V, gg * N * 8, hipMemcpyDeviceToDevice, h->stream));   // Vt (rows >= kk zero)
+            double* T = sw.buf(r * gg);
+            gemm(h, T, r, gg, 1.0, B, N, false, N, V, N, true);                    // B Vt^T (columns >= kk zero)
+            gemm(h, prevk, prow, gg, 1.0, A[k - 1], r, false, r, T, gg, false);
+        }
+        sw.drop(B);
+        sw.drop(A[k - 1]);
+        A[k] = newk;
+        A[k - 1] = prevk;
+        g[k] = gg;
+    }
+
+    // 3. the one synchronisation: statuses, Jacobi sweeps, device ranks
+    int* hs = static_cast<int*>(h->host_scratch) + 12288;
+    XRS_HIP(hipMemcpyAsync(hs, st, size_t(kSlots) * 4, hipMemcpyDeviceToHost, h->stream));
+    host_wait(h);
+    bool ok = true;
+    int bad = -1;
+    for (int i = 0; i < nst; ++i)
+        if (hs[i] != 0) {
+            ok = false;
+            bad = i;
+            break;
+        }
+    int max_sweeps = 0;
+    for (size_t i = 0; i < jac.size(); ++i) {
+        ok = ok && hs[kJac + int(i)] >= 0;
+        max_sweeps = std::max(max_sweeps, hs[kJac + int(i)]);
+    }
+    std::vector<size_t> kk(d + 1, 1);
+    for (size_t k = 1; k < d; ++k) {
+        const int v = hs[kRank + int(k)];
+        ok = ok && v >= 1 && size_t(v) <= g[k];
+        kk[k] = size_t(std::max(v, 1));
+    }
+    if (dbg)
+        std::fprintf(stderr, "round_general: %s (first failing status slot %d), max Jacobi sweeps %d\n", ok ? "certified" : "NOT certified",
+                     bad, max_sweeps);
+    if (!ok) {
+        sw.discard();
+        return false;
+    }
+    // 4. compaction to the device ranks: core_k[:kk_k, :, :kk_{k+1}]
+    std::vector<double*> C(d, nullptr);
+    for (size_t k = 0; k < d; ++k) {
+        const size_t a = kk[k], n = t.n[k], b = kk[k + 1], ga = g[k], gb = g[k + 1];
+        if (a == ga && b == gb) {
+            C[k] = A[k];
+            continue;
+        }
+        C[k] = sw.core(a * n * b);
+        // rows (i, j) of the (ga n) x gb matrix with i < a, first b columns
+        XRS_HIP(hipMemcpy2DAsync(C[k], b * 8, A[k], gb * 8, b * 8, a * n, hipMemcpyDeviceToDevice, h->stream));
+        sw.drop(A[k]);
+    }
+    // right-orthonormality of cores 1..d-1 (S^{-1} U^T B carries kappa(B_kk) u of deviation)
+    {
+        std::vector<const double*> X;
+        std::vector<size_t> m, n;
+        for (size_t k = 1; k < d; ++k) {
+            X.push_back(C[k]);
+            m.push_back(kk[k]);
+            n.push_back(t.n[k] * kk[k + 1]);
+        }
+        orth_devs(sw, X, m, n, true, devb.d());
+    }
+    double* hd = static_cast<double*>(h->host_scratch) + 2048;
+    const int nchk = int(d - 1) * 16;
+    XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
+    host_wait(h);
+    double worst = 0.0;
+    for (int i = 0; i < nchk; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
+    if (dbg) std::fprintf(stderr, "round_general: right orthogonality %.3e\n", worst);
+    if (!(worst <= kTruncAcceptTol)) {
+        sw.discard();
+        return false;
+    }
+    for (size_t k = 0; k < d; ++k) t.replace(k, C[k]);
+    sw.owned.clear();
+    for (size_t k = 1; k < d; ++k) t.r[k] = kk[k];
+    if (worst > kTruncOrthTol) {
+        const bool re = reorthonormalize(t);
+        if (dbg) std::fprintf(stderr, "round_general: re-orthonormalised (%s)\n", re ? "ok" : "failed");
+    }
+    return true;
+}
+
 }  // namespace ttd
 }  // namespace xrs
