@@ -209,6 +209,9 @@ int xrs_tt_dot_wait(xrs_handle_t handle, double* result);
  *  The Python layer (xerus_amd.dist) binds it to torch.distributed (RCCL over xGMI on MI355X).
  *  A NULL hook means one rank: the local sums are final and no synchronisation happens. */
 typedef int (*xrs_allreduce_fn)(void* ctx, double* buf, size_t count);
+/** All-gather: every rank contributes `count` doubles at `send`; `recv` (world * count doubles, device)
+ *  receives them in rank order. Same calling convention as xrs_allreduce_fn. */
+typedef int (*xrs_allgather_fn)(void* ctx, const double* send, double* recv, size_t count);
 
 /** RCCL communicator (no reference counterpart: xerus is single-process). xrs_comm_allreduce is an
  *  xrs_allreduce_fn taking an xrs_comm_t as ctx: it enqueues an in-place fp64 sum ncclAllReduce on the
@@ -222,6 +225,18 @@ int xrs_comm_create(xrs_handle_t handle, int nranks, int rank, const void* id128
 int xrs_comm_destroy(xrs_comm_t comm);
 size_t xrs_comm_calls(xrs_comm_t comm);
 int xrs_comm_allreduce(void* comm, double* buf, size_t count);
+/** xrs_allgather_fn of the communicator: ncclAllGather (fp64) enqueued on the handle's stream. */
+int xrs_comm_allgather(void* comm, const double* send, double* recv, size_t count);
+
+/** Full cores of a mode-sharded TT on every rank (the fallback of a sharded round whose certificate
+ *  fails): the ranks' slices (mode blocks of xerus_amd.dist.mode_partition) of all components go out in
+ *  ONE all-gather of padded blocks and are scattered into new cores (r[k], n_global[k], r[k+1]) from the
+ *  handle's pool (release with xrs_free). Device to device; synchronises. */
+int xrs_tt_gather_sharded(xrs_handle_t handle, size_t d, const size_t* n_global, int world, int rank, const size_t* r,
+                          const double* const* local_cores, double** full_cores_out, xrs_allgather_fn allgather, void* ctx);
+/** This rank's mode slices of full cores into new pool buffers (local_out[k]: (r[k], m_k, r[k+1])). */
+int xrs_tt_shard(xrs_handle_t handle, size_t d, const size_t* n_global, int world, int rank, const size_t* r,
+                 const double* const* full_cores, double** local_out);
 
 /** Mode-sharded TT round (no reference counterpart: xerus is single-process).
  *  Each rank holds, for every component k, the mode slices of its own subset (n_local[k] of them) as

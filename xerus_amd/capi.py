@@ -75,6 +75,10 @@ SIGNATURES = {
     "xrs_comm_destroy": (C.c_int, [_DP]),
     "xrs_comm_calls": (_SZ, [_DP]),
     "xrs_comm_allreduce": (C.c_int, [_DP, _DP, _SZ]),
+    "xrs_comm_allgather": (C.c_int, [_DP, _DP, _DP, _SZ]),
+    "xrs_tt_gather_sharded": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.c_int, C.c_int, C.POINTER(_SZ), C.POINTER(_DP),
+                                        C.POINTER(_DP), _DP, _DP]),
+    "xrs_tt_shard": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.c_int, C.c_int, C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_DP)]),
     "xrs_prof_begin": (C.c_int, [_DP, C.c_uint32]),
     "xrs_prof_end": (C.c_int, [_DP, C.POINTER(_SZ), C.POINTER(C.c_double), C.POINTER(C.c_double),
                                C.POINTER(C.c_double)]),

@@ -27,6 +27,7 @@ struct Rccl {
     decltype(&ncclGetUniqueId) get_unique_id = nullptr;
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
     bool ok = false;
@@ -48,9 +49,10 @@ const Rccl& rccl() {
         x.get_unique_id = reinterpret_cast<decltype(x.get_unique_id)>(dlsym(lib, "ncclGetUniqueId"));
         x.init_rank = reinterpret_cast<decltype(x.init_rank)>(dlsym(lib, "ncclCommInitRank"));
         x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(lib, "ncclAllReduce"));
+        x.all_gather = reinterpret_cast<decltype(x.all_gather)>(dlsym(lib, "ncclAllGather"));
         x.destroy = reinterpret_cast<decltype(x.destroy)>(dlsym(lib, "ncclCommDestroy"));
         x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(lib, "ncclGetErrorString"));
-        x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.destroy && x.error_string;
+        x.ok = x.get_unique_id && x.init_rank && x.all_reduce && x.all_gather && x.destroy && x.error_string;
         if (!x.ok) x.why = "librccl lacks the nccl* entry points";
         return x;
     }();
@@ -116,6 +118,15 @@ int xrs_comm_allreduce(void* ctx, double* buf, size_t count) {
     c->bytes += count * 8;
     if (count == 0) return 0;
     return rccl().all_reduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->h->stream) == ncclSuccess ? 0 : 1;
+}
+
+int xrs_comm_allgather(void* ctx, const double* send, double* recv, size_t count) {
+    auto* c = static_cast<xrs_comm_s*>(ctx);
+    if (!c || !c->comm || (count && !(send && recv))) return 1;
+    ++c->calls;
+    c->bytes += count * 8 * size_t(c->nranks);
+    if (count == 0) return 0;
+    return rccl().all_gather(send, recv, count, ncclDouble, c->comm, c->h->stream) == ncclSuccess ? 0 : 1;
 }
 
 }  // extern "C"

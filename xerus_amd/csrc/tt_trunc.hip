@@ -73,6 +73,7 @@ struct CholJob {
     int n;
     double* L;   // null: certificate only
     double* Z;
+    double shift = 0.0;   // relative diagonal shift (factor jobs; certificates always -kGramShift)
 };
 
 void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
@@ -90,7 +91,7 @@ void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
             continue;
         }
         if (j.n > 256) {
-            big.push_back({j.A, j.L ? 0.0 : -kGramShift, j.n, j.L, j.Z});
+            big.push_back({j.A, j.L ? j.shift : -kGramShift, j.n, j.L, j.Z});
             big_slot.push_back(int(i));
             continue;
         }
@@ -99,7 +100,7 @@ void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
         pb.src[ns] = j.A;
         pb.G[ns] = j.L;
         pb.Dinv[ns] = dinv;
-        pb.shift[ns] = j.L ? 0.0 : -kGramShift;
+        pb.shift[ns] = j.L ? j.shift : -kGramShift;
         pb.n[ns] = j.n;
         ++ns;
         if (j.L && j.Z) {
@@ -125,7 +126,7 @@ void chol_jobs(Sweep& sw, const std::vector<CholJob>& jobs, int* status) {
     int slot = ns + 2 * int(big.size());
     for (int i : huge) {
         const CholJob& j = jobs[size_t(i)];
-        chol_full(h, j.A, size_t(j.n), j.L ? 0.0 : -kGramShift, j.L, j.Z, status + slot);
+        chol_full(h, j.A, size_t(j.n), j.L ? j.shift : -kGramShift, j.L, j.Z, status + slot);
         slot += chol_full_blocks(size_t(j.n));
     }
 }
@@ -179,7 +180,10 @@ __global__ void __launch_bounds__(256) k_edge_factors(const double* __restrict__
 // One left chain pass over the cores `src` (ranks t.r): G_{k+1} = M_k^T (G_k (x) I) M_k, G_k = L_k L_k^T
 // (+ the status-only certificate of G_k - tau tr(G_k) I with `certify`), Z_k = L_k^{-1}, and the
 // left-canonical cores A_k = (L_k^T (x) I) M_k Z_{k+1}^T (A_{d-1} = (L^T (x) I) M_{d-1}).
-void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<double*>& A, int* status, int& nst) {
+// shift: relative diagonal shift of the factorisations (the general round's shifted CholeskyQR3 over the
+// train); Gout / Zout (optional): the Grams G_k and inverses Z_k = L_k^{-1} of this pass (k = 1..d-1)
+void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<double*>& A, int* status, int& nst,
+               double shift = 0.0, std::vector<double*>* Gout = nullptr, std::vector<double*>* Zout = nullptr) {
     TT t = t0;
     t.core = const_cast<double**>(src);
     const size_t d = t.d;
@@ -197,7 +201,7 @@ void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<
         const int a = int(t.r[k]);
         Lf[k] = sw.buf(size_t(a) * a);
         Zf[k] = sw.buf(size_t(a) * a);
-        jobs.push_back({G[k], a, Lf[k], Zf[k]});
+        jobs.push_back({G[k], a, Lf[k], Zf[k], shift});
         if (certify) jobs.push_back({G[k], a, nullptr, nullptr});
     }
     for (size_t b0 = 0; b0 < jobs.size(); b0 += 40) {   // (potrf_batched / trinv tables hold 48 / 64)
@@ -221,6 +225,8 @@ void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<
     }
     gemm_grouped(h, lefts);
     gemm_grouped(h, rights);
+    if (Gout) *Gout = G;
+    if (Zout) *Zout = Zf;
 }
 
 }  // namespace
@@ -415,10 +421,10 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
 //     factor is >= sigma_min, and sigma_min >= 1 / ||R^{-1}||_F, so a device certificate
 //     1 / ||R^{-1}||_F > 32 u ||A||_F proves that no rank drops (else the round falls back);
 //  2. right to left (round_edge, tensorNetwork.cpp:678-818): B = core_k (r x N) = L Q by the same
-//     factorisation (wide), the left singular vectors and values of L by one-sided Jacobi on the rows of
-//     L^T (svd.hip; singular values to u ||B|| absolute, so eps cuts far below sqrt(u) are decided on
+//     factorisation (wide), the right singular vectors and values of L by one-sided Jacobi on its rows
+//     (svd.hip; singular values to u ||B|| absolute, so eps cuts far below sqrt(u) are decided on
 //     accurate values), the cut of calculate_svd (tensor.cpp:1462-1474) evaluated ON THE DEVICE
-//     (k_cut_wide / k_cut_tall), core_k <- S^{-1} U^T B rows, core_{k-1} <- core_{k-1} U S. Ranks are not
+//     (k_cut_rows), core_k <- V_kk^T Q, core_{k-1} <- core_{k-1} L V_kk (= U S). Ranks are not
 //     known on the host until the end: the sweep keeps the uncut sizes with zero rows / columns beyond
 //     the device-side rank, and the cores are compacted once after the single synchronisation.
 // Tall edges (r > N: structural excess at the right end, e.g. x + y) use B = Q R and the right singular
@@ -458,22 +464,8 @@ __device__ int device_cut(const double* __restrict__ S, int r, long max_rank, do
     return best;
 }
 
-// wide edge: Ut (r x r) = U_L^T (rows = left singular vectors of L), S descending. M = S^{-1} Ut rows
-// (r x r, rows >= kk zero): new core = M B; T = Ut^T S (r x r, columns >= kk zero): core_{k-1} <- core_{k-1} T.
-__global__ void __launch_bounds__(256) k_cut_wide(const double* __restrict__ Ut, const double* __restrict__ S, int r, long max_rank,
-                                                  double eps, double* __restrict__ M, double* __restrict__ T, int* __restrict__ kk_out) {
-    const int kk = device_cut(S, r, max_rank, eps);
-    if (blockIdx.x == 0 && threadIdx.x == 0) kk_out[0] = kk;
-    for (int e = blockIdx.x * 256 + threadIdx.x; e < r * r; e += gridDim.x * 256) {
-        const int i = e / r, j = e - i * r;
-        const double u = Ut[e], s = S[i];
-        M[e] = (i < kk && s > 0.0) ? u / s : 0.0;
-        T[size_t(j) * r + i] = i < kk ? u * s : 0.0;
-    }
-}
-
-// tall edge: Vt (g x g) right singular vectors of R (B = Q R); rows >= kk zeroed in place (new core)
-__global__ void __launch_bounds__(256) k_cut_tall(double* __restrict__ Vt, const double* __restrict__ S, int g, long max_rank, double eps,
+// V (g x g): right singular vectors of the edge factor as rows (S descending); rows >= kk zeroed in place
+__global__ void __launch_bounds__(256) k_cut_rows(double* __restrict__ Vt, const double* __restrict__ S, int g, long max_rank, double eps,
                                                   int* __restrict__ kk_out) {
     const int kk = device_cut(S, g, max_rank, eps);
     if (blockIdx.x == 0 && threadIdx.x == 0) kk_out[0] = kk;
@@ -485,6 +477,29 @@ __global__ void __launch_bounds__(256) k_cut_tall(double* __restrict__ Vt, const
 __global__ void k_add_identity(double* __restrict__ X, int n, double v) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) X[size_t(i) * n + i] += v;
+}
+
+// flag = 1 unless 1 / ||W||_F > c ||X||_F with ||X||_F^2 = trace(G) (G: n x n Gram of the unfolding)
+__global__ void __launch_bounds__(256) k_rank_cert_gram(const double* __restrict__ W, const double* __restrict__ G, int n, double c,
+                                                        int* __restrict__ flag) {
+    __shared__ double red[8];
+    double s = 0.0, tr = 0.0;
+    for (int e = threadIdx.x; e < n * n; e += 256) s = fma(W[e], W[e], s);
+    for (int i = threadIdx.x; i < n; i += 256) tr += G[size_t(i) * n + i];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        tr += __shfl_xor(tr, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = s;
+        red[4 + (threadIdx.x >> 6)] = tr;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double w2 = (red[0] + red[1]) + (red[2] + red[3]), t2 = (red[4] + red[5]) + (red[6] + red[7]);
+        flag[0] = (c * c * w2 * t2 < 1.0) ? 0 : 1;
+    }
 }
 
 unsigned grid_for(size_t elems) { return unsigned(std::min<size_t>(std::max<size_t>((elems + 255) / 256, 1), 256)); }
@@ -556,10 +571,87 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
     int nst = 0;
     const int kJac = 1536, kRank = 1792;   // Jacobi sweep counts; device ranks
 
-    // 1. left to right: A_k = Q_k, next = R_k core_{k+1}
     std::vector<double*> A(t.core, t.core + d);   // current cores (originals untouched)
     std::vector<size_t> rr(t.r, t.r + d + 1);
-    for (size_t k = 0; k + 1 < d; ++k) {
+    int* hs = static_cast<int*>(h->host_scratch) + 12288;
+
+    // 1a. left to right as shifted CholeskyQR3 over the whole train: three chain passes (Gram chain
+    //     G_{k+1} = M_k^T (G_k (x) I) M_k, ONE batched Cholesky launch of G_k + s tr(G_k) I (first pass) /
+    //     G_k, grouped transforms A_k = (L_k^T (x) I) M_k L_{k+1}^{-T}) -- the left-orthonormal train
+    //     without a sequential factorisation chain. Per edge R_k = L3^T L2^T L1^T, R_k^{-1} = Z1^T Z2^T Z3^T
+    //     gives the rank certificate; the orthonormality of the result is checked. One synchronisation.
+    bool chain_ok = false;
+    {
+        size_t mmax = 1, rmax = 1;
+        for (size_t k = 0; k < d; ++k) {
+            mmax = std::max(mmax, rr[k] * t.n[k]);
+            rmax = std::max(rmax, rr[k + 1]);
+        }
+        const double s_rel = 11.0 * kUnit * (double(mmax) * double(d) + double(rmax) * double(rmax + 1));
+        std::vector<double*> A1, A2, A3, G1, Z1, Z2, Z3;
+        int cst = 0;
+        left_pass(sw, t, t.core, false, A1, st, cst, s_rel, &G1, &Z1);
+        left_pass(sw, t, A1.data(), false, A2, st, cst, 0.0, nullptr, &Z2);
+        left_pass(sw, t, A2.data(), false, A3, st, cst, 0.0, nullptr, &Z3);
+        for (double* p : A1) sw.drop(p);
+        for (double* p : A2) sw.drop(p);
+        // W_k = Z3 Z2 Z1 (= (R_k^{-1})^T), batched over the edges
+        std::vector<GemmJob> j1, j2;
+        std::vector<double*> W1(d, nullptr), W(d, nullptr);
+        for (size_t k = 1; k < d; ++k) {
+            const size_t a = rr[k];
+            W1[k] = sw.buf(a * a);
+            W[k] = sw.buf(a * a);
+            j1.push_back({a, a, a, a, a, false, false, Z2[k], Z1[k], W1[k]});
+            j2.push_back({a, a, a, a, a, false, false, Z3[k], W1[k], W[k]});
+        }
+        gemm_grouped(h, j1);
+        gemm_grouped(h, j2);
+        const int crank = cst;
+        for (size_t k = 1; k < d; ++k) {
+            hipLaunchKernelGGL(k_rank_cert_gram, dim3(1), dim3(256), 0, h->stream, W[k], G1[k], int(rr[k]), 32.0 * kUnit, st + cst);
+            check_launch("k_rank_cert_gram");
+            ++cst;
+        }
+        {
+            std::vector<const double*> X;
+            std::vector<size_t> m, n;
+            for (size_t k = 0; k + 1 < d; ++k) {
+                X.push_back(A3[k]);
+                m.push_back(rr[k] * t.n[k]);
+                n.push_back(rr[k + 1]);
+            }
+            orth_devs(sw, X, m, n, false, devb.d());
+        }
+        double* hd = static_cast<double*>(h->host_scratch) + 2048;
+        const int nchk = int(d - 1) * 16;
+        XRS_HIP(hipMemcpyAsync(hs, st, size_t(cst) * 4, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
+        host_wait(h);
+        chain_ok = true;
+        int first_bad = -1;
+        for (int i = 0; i < cst; ++i)
+            if (hs[i] != 0) {
+                chain_ok = false;
+                first_bad = i;
+                break;
+            }
+        double worst = 0.0;
+        for (int i = 0; i < nchk; ++i) worst = (hd[i] > worst || hd[i] != hd[i]) ? hd[i] : worst;
+        chain_ok = chain_ok && worst <= kTruncOrthTol;
+        if (dbg)
+            std::fprintf(stderr, "round_general: chain left sweep %s (first bad slot %d of %d, rank certificates from %d), orthogonality %.3e\n",
+                         chain_ok ? "certified" : "NOT certified", first_bad, cst, crank, worst);
+        if (chain_ok) {
+            A = A3;
+        } else {
+            for (double* p : A3) sw.drop(p);
+        }
+        XRS_HIP(hipMemsetAsync(st, 0, size_t(cst) * 4, h->stream));
+    }
+
+    // 1b. otherwise core by core: A_k = Q_k, next = R_k core_{k+1}, each by shifted CholeskyQR3
+    for (size_t k = 0; !chain_ok && k + 1 < d; ++k) {
         const size_t m = rr[k] * t.n[k], b = rr[k + 1];
         XRS_REQUIRE(m >= b, "round_general: structural excess left after the QC steps");
         double* Q = sw.core(m * b);
@@ -574,7 +666,7 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         const size_t cols = t.n[k + 1] * rr[k + 2];
         double* nxt = sw.core(b * cols);
         gemm(h, nxt, b, cols, 1.0, R, b, false, b, A[k + 1], cols, false);
-        if (k > 0) sw.drop(A[k]);   // (an intermediate core of this sweep; the originals are not owned)
+        sw.drop(A[k]);   // (an intermediate core of this sweep; the originals are not owned)
         A[k] = Q;
         A[k + 1] = nxt;
     }
@@ -595,31 +687,26 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         double* S = sw.buf(gg);
         double* V = sw.buf(gg * gg);
         int* js = st + kJac + int(jac.size());
-        // wide: rows of L^T (= the left singular vectors of L); tall: rows of R (its right singular vectors)
-        jacobi_vt(h, F, int(gg), wide, int(gg), int(gg), S, V, int(gg), js);
+        // right singular vectors of the triangular factor by one-sided Jacobi on its rows: accurate to u
+        // whatever the singular value (the left ones would carry u sigma_0 / sigma_j after the division
+        // by S), so the new core V_kk^T Q has orthonormal rows to ~u even after eps cuts far below sqrt(u)
+        jacobi_vt(h, F, int(gg), false, int(gg), int(gg), S, V, int(gg), js);
         jac.push_back(int(k));
+        hipLaunchKernelGGL(k_cut_rows, dim3(grid_for(gg * gg)), dim3(256), 0, h->stream, V, S, int(gg),
+                           long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)), eps, st + kRank + int(k));
+        check_launch("k_cut_rows");   // V rows >= kk zeroed: V_kk^T
         const size_t prow = g[k - 1] * t.n[k - 1];
         double* prevk = sw.core(prow * gg);
-        double* newk;
-        if (wide) {
-            double* M = sw.buf(r * r);
-            double* T = sw.buf(r * r);
-            hipLaunchKernelGGL(k_cut_wide, dim3(grid_for(r * r)), dim3(256), 0, h->stream, V, S, int(r), long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)),
-                               eps, M, T, st + kRank + int(k));
-            check_launch("k_cut_wide");
-            newk = sw.core(r * N);
-            gemm(h, newk, r, N, 1.0, M, r, false, r, B, N, false);                 // S^{-1} U^T B (rows >= kk zero)
-            gemm(h, prevk, prow, r, 1.0, A[k - 1], r, false, r, T, r, false);      // core_{k-1} U S
-        } else {
-            hipLaunchKernelGGL(k_cut_tall, dim3(grid_for(gg * gg)), dim3(256), 0, h->stream, V, S, int(gg),
-                               long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)), eps, st + kRank + int(k));
-            check_launch("k_cut_tall");
-            newk = sw.core(gg * N);
-            XRS_HIP(hipMemcpyAsync(newk, V, gg * N * 8, hipMemcpyDeviceToDevice, h->stream));   // Vt (rows >= kk zero)
-            double* T = sw.buf(r * gg);
-            gemm(h, T, r, gg, 1.0, B, N, false, N, V, N, true);                    // B Vt^T (columns >= kk zero)
-            gemm(h, prevk, prow, gg, 1.0, A[k - 1], r, false, r, T, gg, false);
+        double* newk = sw.core(gg * N);
+        double* T = sw.buf(r * gg);
+        if (wide) {   // B = L Q, L = U S V^T: core_k <- V_kk^T Q, core_{k-1} <- core_{k-1} (L V_kk) = (U S)_kk
+            gemm(h, newk, gg, N, 1.0, V, gg, false, gg, Qf, N, false);
+            gemm(h, T, r, gg, 1.0, F, gg, false, gg, V, gg, true);
+        } else {      // B = Q R, R = U S V^T: core_k <- V_kk^T, core_{k-1} <- core_{k-1} (B V_kk)
+            XRS_HIP(hipMemcpyAsync(newk, V, gg * N * 8, hipMemcpyDeviceToDevice, h->stream));
+            gemm(h, T, r, gg, 1.0, B, N, false, N, V, N, true);
         }
+        gemm(h, prevk, prow, gg, 1.0, A[k - 1], r, false, r, T, gg, false);
         sw.drop(B);
         sw.drop(A[k - 1]);
         A[k] = newk;
@@ -627,8 +714,7 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         g[k] = gg;
     }
 
-    // 3. the one synchronisation: statuses, Jacobi sweeps, device ranks
-    int* hs = static_cast<int*>(h->host_scratch) + 12288;
+    // 3. the synchronisation: statuses, Jacobi sweeps, device ranks
     XRS_HIP(hipMemcpyAsync(hs, st, size_t(kSlots) * 4, hipMemcpyDeviceToHost, h->stream));
     host_wait(h);
     bool ok = true;

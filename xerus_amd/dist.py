@@ -8,8 +8,9 @@ round needs that sums over the mode index -- the left/right Gram chains, the ort
 (``xrs_allreduce_fn``, bound here to torch.distributed: RCCL over xGMI with the "nccl" backend, or
 gloo with host staging); the per-core transforms are purely local. No data-path all-gather is needed.
 
-The product path is the HIP library (xrs_tt_round_sharded / xrs_tt_dot_sharded); the helpers below
-only partition, gather and move bytes.
+The product path is the HIP library (xrs_tt_round_sharded / xrs_tt_dot_sharded); a round whose
+certificate fails gathers the TT device to device (xrs_tt_gather_sharded: one all-gather), rounds it on
+every rank and re-shards locally (ShardedTT.round_any). The helpers below only partition and move bytes.
 """
 from __future__ import annotations
 
@@ -21,6 +22,7 @@ import numpy as np
 from . import capi
 
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 
 def mode_partition(n: int, world: int, rank: int) -> tuple[int, int]:
@@ -90,13 +92,36 @@ class TorchAllReduce:
             except Exception:   # reported to the C side as a failed collective
                 return 1
 
+        def _ag(_ctx, send, recv, count):
+            try:
+                world = self.dist.get_world_size(self.group)
+                ts = self.torch.as_tensor(_CudaArray(int(send), int(count)), device="cuda")
+                tr = self.torch.as_tensor(_CudaArray(int(recv), int(count) * world), device="cuda")
+                if self.device_native:
+                    self.dist.all_gather_into_tensor(tr, ts, group=self.group)
+                else:
+                    parts = [self.torch.empty(int(count), dtype=self.torch.float64) for _ in range(world)]
+                    self.dist.all_gather(parts, ts.cpu(), group=self.group)
+                    tr.copy_(self.torch.cat(parts).to(tr.device))
+                self.torch.cuda.synchronize()
+                self.calls += 1
+                self.bytes += 8 * int(count) * world
+                return 0
+            except Exception:
+                return 1
+
         self.fn = ALLREDUCE_FN(_cb)   # keep a reference: the C side only holds the pointer
+        self.ag = ALLGATHER_FN(_ag)
         self.ctx = None
 
     @property
     def c_fn(self):
         # one rank: no hook at all (the C side then skips the stream synchronisation a hook needs)
         return None if self.single else C.cast(self.fn, C.c_void_p)
+
+    @property
+    def c_ag(self):
+        return None if self.single else C.cast(self.ag, C.c_void_p)
 
 
 class RcclComm:
@@ -125,6 +150,10 @@ class RcclComm:
     @property
     def c_fn(self):
         return C.cast(self.lib.xrs_comm_allreduce, C.c_void_p)
+
+    @property
+    def c_ag(self):
+        return C.cast(self.lib.xrs_comm_allgather, C.c_void_p)
 
     @property
     def ctx(self):
@@ -191,6 +220,39 @@ class ShardedTT:
                     self.handle.lib.xrs_tt_dot_sharded(self.handle.h, C.byref(out), d, capi._arr(x.dims),
                                                        capi._arr(x.r), xc, capi._arr(y.r), yc, comm.c_fn, comm.ctx))
         return out.value
+
+    def gather_device(self, comm) -> capi.TTDevice:
+        """Full cores on every rank, device to device (xrs_tt_gather_sharded: one all-gather of the padded
+        slices of all components over the communicator's all-gather hook)."""
+        t = self.local
+        d = t.order
+        out = (capi._DP * d)()
+        world = self.world if comm.c_ag is not None or self.world > 1 else 1
+        src = (capi._DP * d)(*[capi._DP(p) for p in t.ptrs])
+        capi._check("xrs_tt_gather_sharded",
+                    self.handle.lib.xrs_tt_gather_sharded(self.handle.h, d, capi._arr(self.dims), world, self.rank if world > 1 else 0,
+                                                          capi._arr(t.r), src, out, comm.c_ag, comm.ctx))
+        return capi.TTDevice(self.handle, self.dims, t.r, [p or 0 for p in out[:]], t.canonicalized, t.core_position)
+
+    def round_any(self, max_ranks, comm, eps: float = 8 * np.finfo(float).eps) -> str:
+        """The round for every input: the certified sharded round ("sharded"), else the TT is gathered on the
+        device of every rank, rounded there by the single-GPU round (identical inputs and deterministic
+        kernels: identical results on every rank) and re-sharded locally ("gathered")."""
+        if self.round(max_ranks, comm, eps):
+            return "sharded"
+        full = self.gather_device(comm)
+        full.round(max_ranks, eps)
+        d = full.order
+        src = (capi._DP * d)(*[capi._DP(p) for p in full.ptrs])
+        out = (capi._DP * d)()
+        capi._check("xrs_tt_shard", self.handle.lib.xrs_tt_shard(self.handle.h, d, capi._arr(self.dims), self.world, self.rank,
+                                                                 capi._arr(full.r), src, out))
+        local_dims = [mode_partition(n, self.world, self.rank)[1] for n in self.dims]
+        new = capi.TTDevice(self.handle, local_dims, full.r, [p or 0 for p in out[:]], True, 0)
+        full.free()
+        self.local.free()
+        self.local = new
+        return "gathered"
 
     def gather(self, all_gather_object: Callable) -> list[np.ndarray]:
         """Full cores on every rank (all_gather_object: torch.distributed.all_gather_object-like)."""
