@@ -73,6 +73,9 @@ def _worker(rank, world, port, backend, hook, out):
             res["ref_ranks"] = xr.ranks
             res["diff"] = _rel_diff(ref, full, x.cores)
             # right-canonical: cores 1.. have orthonormal rows
+            xs = ref.tt_add(x, x)
+            xs.round(100)
+            res["ref_ranks_sum"] = xs.ranks
             res["orth"] = max(np.abs(c.reshape(c.shape[0], -1) @ c.reshape(c.shape[0], -1).T - np.eye(c.shape[0])).max()
                               for c in full[1:])
         # doubled ranks (x + x): certificate must fail, cores untouched
@@ -82,6 +85,17 @@ def _worker(rank, world, port, backend, hook, out):
         res["cert_sum"] = ss.round(100, comm)
         after = ss.local.cores()
         res["untouched"] = all(np.array_equal(a, b) for a, b in zip(before, after))
+        # ... and round_any completes it: device all-gather (xrs_tt_gather_sharded), the single-GPU round on
+        # every rank, local re-shard (xrs_tt_shard); gather_device of the result on every rank
+        res["any_path"] = ss.round_any(100, comm)
+        res["any_ranks"] = ss.ranks
+        g_full = ss.gather_device(comm)
+        res["any_full"] = g_full.cores() if rank == 0 else None
+        g_full.free()
+        # device gather of an untouched sharded TT reproduces the full cores bit for bit
+        gx = xd.ShardedTT.from_full_cores(h, y.cores, world, rank).gather_device(comm)
+        res["gather_exact"] = all(np.array_equal(a, b) for a, b in zip(gx.cores(), y.cores))
+        gx.free()
         # truncating sharded round (ranks 12 -> 8): the certified truncation with all-reduced Grams
         st = xd.ShardedTT.from_full_cores(h, x.cores, world, rank)
         res["cert_trunc"] = st.round(8, comm)
@@ -127,7 +141,15 @@ def test_sharded_round_and_dot(world, backend, hook):
         assert r["cert"] is True
         assert r["ranks"] == r0["ref_ranks"]
         assert r["cert_sum"] is False and r["untouched"]
+        assert r["any_path"] == "gathered"
+        assert r["any_ranks"] == r0["ref_ranks_sum"]
+        assert r["gather_exact"]
     assert r0["diff"] <= 1e-12
+    from oracle import xerus_ref as ref
+    from ttutil import tt_diff_norm
+    x = ref.TT.random_raw([8, 6, 7, 5, 8, 6], [6, 12, 12, 10, 6], ref.Rng(31))
+    e, nrm = tt_diff_norm(r0["any_full"], [2 * c if k == 0 else c for k, c in enumerate(x.cores)])
+    assert e <= 1e-12 * nrm
     assert r0["orth"] <= 1e-13
     assert r0["calls"] > 0
     for rank in range(world):

@@ -159,3 +159,37 @@ def test_svd_rows_vt_rank_deficient(handle, kernel):
     assert np.max(np.abs(S[7:])) <= 1e-12 * ref[0]
     Vt7 = Vt.numpy()[:7]
     assert np.linalg.norm(Vt7 @ Vt7.T - np.eye(7)) <= 1e-13
+
+
+@pytest.mark.parametrize("m,n,k", [(600, 600, 300), (1024, 700, 650), (700, 1024, 600)])
+def test_qc_cq_rank_deficient_above_512(handle, ref, m, n, k):
+    """Rank-revealing QC / CQ of rank-deficient matrices with min(m, n) > 512: shifted CholeskyQR3 breaks
+    down, the exact dgeqp3 emulation runs on the matrix itself; the rank is the reference's rule
+    (blasLapackWrapper.cpp:268-272, oracle: LAPACK dgeqp3)."""
+    rng = np.random.default_rng(m + n + k)
+    A = rng.standard_normal((m, k)) @ rng.standard_normal((k, n))
+    Q, Cm, r = handle.qc(handle.array(A))
+    assert r == ref.qc(A)[2] == k
+    assert _rel(Q.numpy() @ Cm.numpy(), A) <= 1e-11
+    Cc, Qc, r2 = handle.cq(handle.array(A))
+    assert r2 == ref.cq(A)[2] == k
+    assert _rel(Cc.numpy() @ Qc.numpy(), A) <= 1e-11
+    Qh = Qc.numpy()
+    assert np.abs(Qh @ Qh.T - np.eye(r2)).max() <= 1e-12
+
+
+@pytest.mark.parametrize("m,n", [(600, 600), (900, 700), (700, 1024), (1024, 1024), (3000, 600)])
+def test_svd_above_512(handle, ref, m, n):
+    """The API SVD for 512 < min(m, n) <= 1024 (QR preconditioning + block Jacobi on the triangular factor):
+    singular values vs dgesdd, reconstruction and orthogonality at LAPACK level."""
+    A = np.random.default_rng(m * 3 + n).standard_normal((m, n))
+    A[:, : min(m, n) // 3] *= 1e-4   # a graded part
+    U, S, Vt = handle.svd(handle.array(A))
+    Uh, Sh, Vh = U.numpy(), S.numpy(), Vt.numpy()
+    Sr = ref.svd(A)[1]
+    k = min(m, n)
+    assert np.all(np.diff(Sh) <= 0)
+    assert np.max(np.abs(Sh - Sr)) <= 1e-12 * Sr[0]
+    assert _rel((Uh * Sh[None, :]) @ Vh, A) <= 1e-13
+    assert np.abs(Uh.T @ Uh - np.eye(k)).max() <= 1e-12
+    assert np.abs(Vh @ Vh.T - np.eye(k)).max() <= 1e-12

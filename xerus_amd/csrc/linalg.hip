@@ -209,7 +209,8 @@ static OrthResult orthogonalize_big(xrs_handle_t h, const double* A, size_t m, s
         gram(T.d(), Q);
         if (max_abs_dev_identity(h, T.d(), N) <= 64.0 * double(N) * kU) return res;
     }
-    throw Error{XRS_ENUMERIC, "orthogonalize: a numerically rank-deficient matrix with rank > 512 is not supported"};
+    // (qc / cq / qr / rq catch this and run the exact Householder emulation on the matrix itself)
+    throw Error{XRS_ENUMERIC, "orthogonalize: a numerically rank-deficient matrix above 512 (shifted CholeskyQR3 failed)"};
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -325,17 +326,23 @@ static void compact_cols(xrs_handle_t h, double* dst, size_t ldd, const double* 
 size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* C) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     const size_t k = std::min(m, n);
-    if (m < n || small_problem(m, n)) {
+    auto exact = [&] {   // the dgeqp3 emulation on A itself
         DevBuf Qf(h, m * k * 8);
         const size_t r = qrcp(h, A, m, n, Qf.d(), C, true, false, true);
         compact_cols(h, Q, r, Qf.d(), k, m, r);
         return r;
+    };
+    if (m < n || small_problem(m, n)) return exact();
+    OrthResult o;
+    try {
+        o = orthogonalize(h, A, m, n, false, Q, C);
+    } catch (const Error& e) {   // above 512: numerically rank-deficient beyond shifted CholeskyQR3
+        if (e.code != XRS_ENUMERIC) throw;
+        return exact();
     }
-    OrthResult o = orthogonalize(h, A, m, n, false, Q, C);
     // certified: sigma_min >= cert*||A||_F > 16 u R_00 (R_00 <= ||A||_F) -> rank n
     if (o.certified && o.cert_ratio > 64.0 * kDblEps) return n;
     if (!reference_r00_positive(h, A, m, n, false)) return n;  // reference never reduces rank then
-    XRS_REQUIRE(n <= size_t(kSmallMax), "qc: the rank-revealing pivoted QR above 512 columns is not supported");
     // exact pivoted rank on the triangular factor (same column norms as A up to rounding)
     DevBuf Rc(h, n * n * 8), Q2(h, n * n * 8), Cq(h, n * n * 8), Qo(h, m * n * 8);
     XRS_HIP(hipMemcpyAsync(Rc.d(), C, n * n * 8, hipMemcpyDeviceToDevice, h->stream));
@@ -350,7 +357,7 @@ size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double
 size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double* Q) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     const size_t k = std::min(m, n);
-    if (n < m || small_problem(m, n)) {
+    auto exact = [&] {
         DevBuf At(h, m * n * 8), Qt(h, n * k * 8), Ct(h, k * m * 8);
         transpose(h, At.d(), A, m, n);                           // n x m
         const size_t r = qrcp(h, At.d(), n, m, Qt.d(), Ct.d(), true, false, true);   // A^T = Qt Ct
@@ -359,11 +366,17 @@ size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double
         transpose(h, Q, Qc.d(), n, r);                            // Q = Qt^T  (r x n)
         transpose(h, C, Ct.d(), r, m);                            // C = Ct^T  (m x r)
         return r;
+    };
+    if (n < m || small_problem(m, n)) return exact();
+    OrthResult o;
+    try {
+        o = orthogonalize(h, A, m, n, true, Q, C);               // A = L Q, C := L (m x m)
+    } catch (const Error& e) {
+        if (e.code != XRS_ENUMERIC) throw;
+        return exact();
     }
-    OrthResult o = orthogonalize(h, A, m, n, true, Q, C);        // A = L Q, C := L (m x m)
     if (o.certified && o.cert_ratio > 64.0 * kDblEps) return m;
     if (!reference_r00_positive(h, A, m, n, true)) return m;
-    XRS_REQUIRE(m <= size_t(kSmallMax), "cq: the rank-revealing pivoted QR above 512 rows is not supported");
     DevBuf Lt(h, m * m * 8), Q2(h, m * m * 8), C2(h, m * m * 8), Qo(h, m * n * 8);
     transpose(h, Lt.d(), C, m, m);                                // A^T = Q^T L^T
     const size_t r = qrcp(h, Lt.d(), m, m, Q2.d(), C2.d(), true, true, true);   // L^T P = Q2 R2
@@ -376,8 +389,12 @@ size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double
 void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* R) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     if (m >= n && !small_problem(m, n)) {
-        orthogonalize(h, A, m, n, false, Q, R);
-        return;
+        try {
+            orthogonalize(h, A, m, n, false, Q, R);
+            return;
+        } catch (const Error& e) {   // rank-deficient above 512: the exact dgeqrf emulation
+            if (e.code != XRS_ENUMERIC) throw;
+        }
     }
     qrcp(h, A, m, n, Q, R, false, false, false);
 }
@@ -385,8 +402,12 @@ void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* 
 void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* Q) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
     if (m <= n && !small_problem(m, n)) {
-        orthogonalize(h, A, m, n, true, Q, R);
-        return;
+        try {
+            orthogonalize(h, A, m, n, true, Q, R);
+            return;
+        } catch (const Error& e) {
+            if (e.code != XRS_ENUMERIC) throw;
+        }
     }
     const size_t k = std::min(m, n);
     DevBuf At(h, m * n * 8), Qt(h, n * k * 8), Rt(h, k * m * 8);
@@ -396,9 +417,50 @@ void rq(xrs_handle_t h, const double* A, size_t m, size_t n, double* R, double* 
     transpose(h, R, Rt.d(), k, m);
 }
 
+// U[:, j] *= 1 / S[j] (0 for S[j] == 0): U = R V S^{-1}
+__global__ void k_div_cols(double* __restrict__ U, const double* __restrict__ S, size_t m, size_t k) {
+    for (size_t e = size_t(blockIdx.x) * blockDim.x + threadIdx.x; e < m * k; e += size_t(gridDim.x) * blockDim.x) {
+        const double s = S[e % k];
+        U[e] = s > 0.0 ? U[e] / s : 0.0;
+    }
+}
+
+// 512 < min(m, n) <= 1024: tall A = Q R (shifted CholeskyQR3), the right singular vectors of R by the
+// multi-workgroup block Jacobi on its rows (accurate to u for every singular value), U = Q R V S^{-1}
+// re-orthonormalised by CholeskyQR (its columns of tiny singular values carry u sigma_0 / sigma_j;
+// the re-orthonormalisation keeps U S Vt = A to u ||A||). Wide A through A^T.
+static void svd_big(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
+    if (m < n) {
+        DevBuf At(h, m * n * 8), U2(h, n * m * 8), V2(h, m * m * 8);
+        transpose(h, At.d(), A, m, n);                 // n x m, tall
+        svd_big(h, At.d(), n, m, U2.d(), S, V2.d());   // A^T = U2 S V2t
+        transpose(h, U, V2.d(), m, m);                  // U = V2t^T (m x m)
+        transpose(h, Vt, U2.d(), n, m);                 // Vt = U2^T (m x n)
+        return;
+    }
+    XRS_REQUIRE(n <= 1024, "svd: min(m, n) > 1024 not supported");
+    DevBuf Q(h, m * n * 8), R(h, n * n * 8), Ur(h, n * n * 8), Uq(h, m * n * 8), Rn(h, n * n * 8), st(h, 64);
+    orthogonalize(h, A, m, n, false, Q.d(), R.d());
+    XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
+    jacobi_vt(h, R.d(), int(n), false, int(n), int(n), S, Vt, int(n), st.as<int>(), 60);
+    gemm(h, Ur.d(), n, n, 1.0, R.d(), n, false, n, Vt, n, true);   // R V = U_R S
+    hipLaunchKernelGGL(k_div_cols, dim3(unsigned(std::min<size_t>((n * n + 255) / 256, 4096))), dim3(256), 0, h->stream, Ur.d(), S, n, n);
+    check_launch("k_div_cols");
+    gemm(h, Uq.d(), m, n, 1.0, Q.d(), n, false, n, Ur.d(), n, false);   // Q U_R
+    orthogonalize(h, Uq.d(), m, n, false, U, Rn.d());
+    int sw = 0;
+    read_status(h, st.as<int>(), 1, &sw);
+    if (sw < 0)
+        std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %zu x %zu matrix did not converge (status %d)\n", n, n,
+                     sw);
+}
+
 void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
-    XRS_REQUIRE(std::min(m, n) <= size_t(kSmallMax), "svd: min(m, n) > 512 not supported yet");
+    if (std::min(m, n) > size_t(kSmallMax)) {
+        svd_big(h, A, m, n, U, S, Vt);
+        return;
+    }
     if (m <= n && jacobi_usv_fits(int(m), int(n))) {
         jacobi_svd_rows(h, A, int(m), int(n), U, S, Vt);   // rows of A directly
         return;

@@ -125,74 +125,64 @@ size_t svd_cut(const std::vector<double>& s, size_t max_rank, double eps) {
     return rank;
 }
 
-// S[i] = max(0, S[i] - soft) for the kept i < kk (round_edge's soft threshold, tensorNetwork.cpp:766, 788)
-__global__ void k_soft_shift(double* __restrict__ S, int kk, double soft) {
-    for (int i = threadIdx.x; i < kk; i += blockDim.x) S[i] = fmax(0.0, S[i] - soft);
+// T[:, j] *= ratio_j = max(0, S_j - soft) / S_j (0 for S_j == 0): (U S) -> (U S') with the soft threshold
+__global__ void k_soft_cols(double* __restrict__ T, const double* __restrict__ S, size_t rows, size_t cols, double soft) {
+    for (size_t e = size_t(blockIdx.x) * blockDim.x + threadIdx.x; e < rows * cols; e += size_t(gridDim.x) * blockDim.x) {
+        const double s = S[e % cols];
+        T[e] = s > 0.0 ? T[e] * (fmax(0.0, s - soft) / s) : 0.0;
+    }
 }
 
-static void soft_shift(xrs_handle_t h, double* S, size_t kk, double soft) {
-    if (!(soft > 0.0) || kk == 0) return;
-    hipLaunchKernelGGL(k_soft_shift, dim3(1), dim3(256), 0, h->stream, S, int(kk), soft);
-    check_launch("k_soft_shift");
-}
-
-// truncate the edge between core k-1 and core k (round_edge(k, k-1), core moves to k-1)
+// truncate the edge between core k-1 and core k (round_edge(k, k-1), core moves to k-1):
+// B = core_k (m x nn) = L Q (wide) or Q R (tall), F the triangular factor (g x g, g = min(m, nn) <= 1024),
+// F = U S V^T with V from one-sided Jacobi on the rows of F (accurate to u for every singular value);
+// the reference's cut (tensor.cpp:1462-1474) on S; core_k <- V_kk^T Q (wide) / V_kk^T (tall),
+// core_{k-1} <- core_{k-1} (F V_kk) / (B V_kk) = core_{k-1} (U S)_kk, with max(0, S - soft) for soft > 0
 void truncate_edge(TT& t, size_t k, size_t max_rank, double eps, double soft) {
     const size_t m = t.r[k], nn = t.cols_right(k);
     const size_t prow = t.rows_left(k - 1);
     xrs_handle_t h = t.h;
-    if (m <= nn && m <= size_t(kSmallMax)) {
-        double* Q = t.alloc(m * nn);
-        double* L = t.alloc(m * m);
-        const OrthResult o = orthogonalize(h, t.core[k], m, nn, true, Q, L);
-        if (o.certified && eps < 0.5 * o.cert_ratio && max_rank >= m && !(soft > 0.0)) {
-            double* prv = t.alloc(prow * m);
-            gemm(h, prv, prow, m, 1.0, t.core[k - 1], m, false, m, L, m, false);
-            t.release(L);
-            t.replace(k, Q);
-            t.replace(k - 1, prv);
-            return;
-        }
-        // SVD of the r x r factor: L = U S Vt  ->  B = U S (Vt Q)
-        DevBuf U(h, m * m * 8), S(h, m * 8), Vt(h, m * m * 8);
-        jacobi_svd_rows(h, L, int(m), int(m), U.d(), S.d(), Vt.d());
-        std::vector<double> s(m);
-        XRS_HIP(hipMemcpyAsync(s.data(), S.d(), m * 8, hipMemcpyDeviceToHost, h->stream));
-        XRS_HIP(hipStreamSynchronize(h->stream));
-        const size_t kk = svd_cut(s, max_rank, eps);
-        soft_shift(h, S.d(), kk, soft);
-        double* cur = t.alloc(kk * nn);
-        gemm(h, cur, kk, nn, 1.0, Vt.d(), m, false, m, Q, nn, false);          // Vt[:kk] Q
-        scale_cols(h, U.d(), S.d(), m, m);                                     // U S (columns >= kk unused)
-        double* prv = t.alloc(prow * kk);
-        gemm(h, prv, prow, kk, 1.0, t.core[k - 1], m, false, m, U.d(), m, false);  // prev * (U S)[:, :kk]
-        t.release(L);
-        t.release(Q);
-        t.replace(k, cur);
+    const bool wide = m <= nn;
+    const size_t g = wide ? m : nn;
+    XRS_REQUIRE(g <= kHugeMax, "TT round: an edge whose unfoldings both exceed 1024 is not supported");
+    double* Q = t.alloc(m * nn);
+    double* F = t.alloc(g * g);
+    const OrthResult o = orthogonalize(h, t.core[k], m, nn, wide, Q, F);
+    if (wide && o.certified && eps < 0.5 * o.cert_ratio && max_rank >= m && !(soft > 0.0)) {
+        double* prv = t.alloc(prow * m);   // no singular value can be cut: B = L Q directly
+        gemm(h, prv, prow, m, 1.0, t.core[k - 1], m, false, m, F, m, false);
+        t.release(F);
+        t.replace(k, Q);
         t.replace(k - 1, prv);
-        t.r[k] = kk;
         return;
     }
-    // tall unfolding (r_k > n_k r_{k+1}) or rank > 512: B = Q R, SVD of R, B = (Q U) S Vt
-    XRS_REQUIRE(nn <= size_t(kSmallMax), "TT round: unfolding with both sides > 512 not supported yet");
-    double* Q = t.alloc(m * nn);
-    double* R = t.alloc(nn * nn);
-    orthogonalize(h, t.core[k], m, nn, false, Q, R);
-    DevBuf U(h, nn * nn * 8), S(h, nn * 8), Vt(h, nn * nn * 8), QU(h, m * nn * 8);
-    jacobi_svd_rows(h, R, int(nn), int(nn), U.d(), S.d(), Vt.d());
-    std::vector<double> s(nn);
-    XRS_HIP(hipMemcpyAsync(s.data(), S.d(), nn * 8, hipMemcpyDeviceToHost, h->stream));
-    XRS_HIP(hipStreamSynchronize(h->stream));
+    DevBuf S(h, g * 8), Vt(h, g * g * 8), st(h, 64);
+    XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
+    jacobi_vt(h, F, int(g), false, int(g), int(g), S.d(), Vt.d(), int(g), st.as<int>(), 60);
+    std::vector<double> s(g);
+    XRS_HIP(hipMemcpyAsync(s.data(), S.d(), g * 8, hipMemcpyDeviceToHost, h->stream));
+    int sweeps = 0;
+    read_status(h, st.as<int>(), 1, &sweeps);   // (synchronises, s is on the host too)
+    if (sweeps < 0)   // non-convergence is a warning, as the reference's dgesdd failure (blasLapackWrapper.cpp:216-224)
+        std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %zu x %zu matrix did not converge (status %d)\n", g, g,
+                     sweeps);
     const size_t kk = svd_cut(s, max_rank, eps);
-    soft_shift(h, S.d(), kk, soft);
+    double* T = t.alloc(m * kk);
+    if (wide) gemm(h, T, m, kk, 1.0, F, g, false, g, Vt.d(), g, true);          // L V_kk = (U S)_kk
+    else gemm(h, T, m, kk, 1.0, t.core[k], nn, false, nn, Vt.d(), g, true);     // B V_kk
+    if (soft > 0.0) {
+        hipLaunchKernelGGL(k_soft_cols, dim3(unsigned(std::min<size_t>((m * kk + 255) / 256, 4096))), dim3(256), 0, h->stream, T, S.d(), m, kk,
+                           soft);
+        check_launch("k_soft_cols");
+    }
     double* cur = t.alloc(kk * nn);
-    XRS_HIP(hipMemcpyAsync(cur, Vt.d(), kk * nn * 8, hipMemcpyDeviceToDevice, h->stream));
-    gemm(h, QU.d(), m, nn, 1.0, Q, nn, false, nn, U.d(), nn, false);
-    scale_cols(h, QU.d(), S.d(), m, nn);
+    if (wide) gemm(h, cur, kk, nn, 1.0, Vt.d(), g, false, g, Q, nn, false);     // V_kk^T Q
+    else XRS_HIP(hipMemcpyAsync(cur, Vt.d(), kk * nn * 8, hipMemcpyDeviceToDevice, h->stream));
     double* prv = t.alloc(prow * kk);
-    gemm(h, prv, prow, kk, 1.0, t.core[k - 1], m, false, m, QU.d(), nn, false);
+    gemm(h, prv, prow, kk, 1.0, t.core[k - 1], m, false, m, T, kk, false);
+    t.release(T);
+    t.release(F);
     t.release(Q);
-    t.release(R);
     t.replace(k, cur);
     t.replace(k - 1, prv);
     t.r[k] = kk;
