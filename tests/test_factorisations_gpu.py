@@ -167,15 +167,25 @@ def test_qc_cq_rank_deficient_above_512(handle, ref, m, n, k):
     down, the exact dgeqp3 emulation runs on the matrix itself; the rank is the reference's rule
     (blasLapackWrapper.cpp:268-272, oracle: LAPACK dgeqp3)."""
     rng = np.random.default_rng(m + n + k)
-    A = rng.standard_normal((m, k)) @ rng.standard_normal((k, n))
-    Q, Cm, r = handle.qc(handle.array(A))
-    assert r == ref.qc(A)[2] == k
-    assert _rel(Q.numpy() @ Cm.numpy(), A) <= 1e-11
-    Cc, Qc, r2 = handle.cq(handle.array(A))
-    assert r2 == ref.cq(A)[2] == k
-    assert _rel(Cc.numpy() @ Qc.numpy(), A) <= 1e-11
-    Qh = Qc.numpy()
-    assert np.abs(Qh @ Qh.T - np.eye(r2)).max() <= 1e-12
+    A0 = rng.standard_normal((m, k)) @ rng.standard_normal((k, n))
+    # The reference cuts only when its R_00 is positive (|R_kk| < 16 eps R_00, R_00 signed), i.e. for one of
+    # A and -A: both signs are run, so the cut and the no-cut branch of the rule are each exercised once.
+    qc_ranks, cq_ranks = set(), set()
+    for sign in (1.0, -1.0):
+        A = sign * A0
+        Q, Cm, r = handle.qc(handle.array(A))
+        assert r == ref.qc(A)[2]
+        qc_ranks.add(r)
+        assert _rel(Q.numpy() @ Cm.numpy(), A) <= 1e-11
+        Cc, Qc, r2 = handle.cq(handle.array(A))
+        assert r2 == ref.cq(A)[2]
+        cq_ranks.add(r2)
+        assert _rel(Cc.numpy() @ Qc.numpy(), A) <= 1e-11
+        Qh = Qc.numpy()
+        assert np.abs(Qh @ Qh.T - np.eye(r2)).max() <= 1e-12
+    # the cut branch keeps k (or k + 1: an R_kk of the rank-k product can sit just above 16 eps R_00)
+    for ranks in (qc_ranks, cq_ranks):
+        assert len(ranks) == 2 and max(ranks) == min(m, n) and k <= min(ranks) <= k + 1, ranks
 
 
 @pytest.mark.parametrize("m,n", [(600, 600), (900, 700), (700, 1024), (1024, 1024), (3000, 600)])

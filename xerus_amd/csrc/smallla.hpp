@@ -65,6 +65,10 @@ bool jacobi_vt_fits_lds(int p, int q);
 bool jacobi_usv_fits(int p, int q);
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
                 int* status_dev, int max_sweeps = 40);
+// Right singular vectors (rows of Vt, g x g) and S of a triangular g x g factor F: lower (L of B = L Q) by
+// accumulated rotations on the rows of F^T, upper (R of B = Q R) on the rows of F. Enqueued only.
+void jacobi_right_vectors(xrs_handle_t h, const double* F, int g, bool lower, double* S, double* Vt, int* status_dev,
+                          int max_sweeps = 40);
 
 struct OrthResult {
     bool certified;   // sigma_min(A) >= cert_ratio * ||A||_F proven (Cholesky of the shifted Gram succeeded)

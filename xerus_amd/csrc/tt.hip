@@ -135,7 +135,8 @@ __global__ void k_soft_cols(double* __restrict__ T, const double* __restrict__ S
 
 // truncate the edge between core k-1 and core k (round_edge(k, k-1), core moves to k-1):
 // B = core_k (m x nn) = L Q (wide) or Q R (tall), F the triangular factor (g x g, g = min(m, nn) <= 1024),
-// F = U S V^T with V from one-sided Jacobi on the rows of F (accurate to u for every singular value);
+// F = U S V^T with V from one-sided Jacobi (jacobi_right_vectors: accumulated rotations on the columns of a
+// wide L, the rows of a tall R; accurate to u for every singular value);
 // the reference's cut (tensor.cpp:1462-1474) on S; core_k <- V_kk^T Q (wide) / V_kk^T (tall),
 // core_{k-1} <- core_{k-1} (F V_kk) / (B V_kk) = core_{k-1} (U S)_kk, with max(0, S - soft) for soft > 0
 void truncate_edge(TT& t, size_t k, size_t max_rank, double eps, double soft) {
@@ -158,7 +159,7 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps, double soft) {
     }
     DevBuf S(h, g * 8), Vt(h, g * g * 8), st(h, 64);
     XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
-    jacobi_vt(h, F, int(g), false, int(g), int(g), S.d(), Vt.d(), int(g), st.as<int>(), 60);
+    jacobi_right_vectors(h, F, int(g), wide, S.d(), Vt.d(), st.as<int>(), 60);
     std::vector<double> s(g);
     XRS_HIP(hipMemcpyAsync(s.data(), S.d(), g * 8, hipMemcpyDeviceToHost, h->stream));
     int sweeps = 0;

@@ -687,10 +687,11 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         double* S = sw.buf(gg);
         double* V = sw.buf(gg * gg);
         int* js = st + kJac + int(jac.size());
-        // right singular vectors of the triangular factor by one-sided Jacobi on its rows: accurate to u
-        // whatever the singular value (the left ones would carry u sigma_0 / sigma_j after the division
-        // by S), so the new core V_kk^T Q has orthonormal rows to ~u even after eps cuts far below sqrt(u)
-        jacobi_vt(h, F, int(gg), false, int(gg), int(gg), S, V, int(gg), js);
+        // right singular vectors of the triangular factor by one-sided Jacobi (svd.hip jacobi_right_vectors:
+        // wide L through its columns with the rotations accumulated, tall R through its rows): accurate to u
+        // whatever the singular value (no division by S), so the new core V_kk^T Q has orthonormal rows to
+        // ~u even after eps cuts far below sqrt(u)
+        jacobi_right_vectors(h, F, int(gg), wide, S, V, js);
         jac.push_back(int(k));
         hipLaunchKernelGGL(k_cut_rows, dim3(grid_for(gg * gg)), dim3(256), 0, h->stream, V, S, int(gg),
                            long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)), eps, st + kRank + int(k));
@@ -736,9 +737,12 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         ok = ok && v >= 1 && size_t(v) <= g[k];
         kk[k] = size_t(std::max(v, 1));
     }
-    if (dbg)
-        std::fprintf(stderr, "round_general: %s (first failing status slot %d), max Jacobi sweeps %d\n", ok ? "certified" : "NOT certified",
+    if (dbg) {
+        std::fprintf(stderr, "round_general: %s (first failing status slot %d), max Jacobi sweeps %d; per edge:", ok ? "certified" : "NOT certified",
                      bad, max_sweeps);
+        for (size_t i = 0; i < jac.size(); ++i) std::fprintf(stderr, " %d:%d", jac[i], hs[kJac + int(i)]);
+        std::fprintf(stderr, "\n");
+    }
     if (!ok) {
         sw.discard();
         return false;
