@@ -10,6 +10,8 @@
 #include "xerus/tensorNetwork.h"
 #include "xerus/ttNetwork.h"
 #include "xerus/algorithms/als.h"
+#include "xerus/measurments.h"
+#include "xerus/algorithms/adf.h"
 
 namespace xerus {
 namespace gpu {

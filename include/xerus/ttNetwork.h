@@ -59,6 +59,8 @@ class TTTensor {
         return result;
     }
     static std::vector<size_t> reduce_to_maximal_ranks(std::vector<size_t> _ranks, const std::vector<size_t>& _dimensions);
+    /// all-ones rank-1 TT, then canonicalize_left (ttNetwork.cpp:170-191)
+    static TTTensor ones(const std::vector<size_t>& _dimensions);
 
     size_t degree() const { return dimensions.size(); }
     std::vector<size_t> ranks() const;

@@ -769,3 +769,146 @@ def dmrg(A: Sequence[np.ndarray], x: TT, b: TT, spd: bool = True, num_half_sweep
             bL.pop()
             bR.append(rhs_right(bR[-1], cur + s - 1))
             cur -= 1
+
+
+# ------------------------------------------------------------------------------------------------
+# Measurement sets and ADF (measurments.cpp, algorithms/adf.cpp). Test infrastructure: the reference's
+# algorithm on numpy, with every stack entry computed per measurement (the reference's de-duplication of
+# equal position prefixes, adf.cpp:102-191, shares identical products and changes no value).
+def uniform_index(rng: Rng, n: int) -> int:
+    """libstdc++ std::uniform_int_distribution<size_t>(0, n - 1)(mt19937_64): the 'downscaling' branch
+    (urng range 2^64 - 1 > n - 1): scaling = (2^64 - 1) // n, reject draws >= n * scaling, then divide."""
+    urngrange = (1 << 64) - 1
+    scaling = urngrange // n
+    past = n * scaling
+    while True:
+        v = int(_lib().orc_rng_next(rng._state))
+        if v < past:
+            return v // scaling
+
+
+def sp_random_positions(rng: Rng, num: int, dims: Sequence[int]) -> np.ndarray:
+    """SinglePointMeasurementSet::create_random_positions (measurments.cpp:211-236): distinct multi-indices
+    drawn mode by mode, then sorted lexicographically."""
+    seen, pos = set(), []
+    while len(pos) < num:
+        idx = [uniform_index(rng, int(n)) for n in dims]
+        lin = 0
+        for i, n in zip(idx, dims):
+            lin = lin * int(n) + i
+        if lin not in seen:
+            seen.add(lin)
+            pos.append(idx)
+    pos.sort()
+    return np.asarray(pos, dtype=np.int64).reshape(num, len(dims))
+
+
+def tt_measure_sp(x: TT, pos: np.ndarray) -> np.ndarray:
+    """x[positions] (SinglePointMeasurementSet::measure(TensorNetwork), measurments.cpp:120-148)."""
+    F = np.ones((pos.shape[0], 1))
+    for k, C in enumerate(x.cores):
+        F = np.einsum("ma,amb->mb", F, C[:, pos[:, k], :])
+    return F[:, 0]
+
+
+def tt_measure_r1(x: TT, vecs: Sequence[np.ndarray]) -> np.ndarray:
+    """<x, v_0 (x) ... (x) v_{d-1}> per measurement (RankOneMeasurementSet::measure, measurments.cpp:393-420)."""
+    F = np.ones((vecs[0].shape[0], 1))
+    for k, C in enumerate(x.cores):
+        F = np.einsum("ma,mt,atb->mb", F, vecs[k], C)
+    return F[:, 0]
+
+
+def adf(x: TT, values: np.ndarray, max_ranks: Sequence[int], positions: np.ndarray | None = None,
+        vectors: Sequence[np.ndarray] | None = None, max_iterations: int = 0, target: float = 1e-8,
+        min_decrease: float = 0.999, rng: Rng | None = None) -> float:
+    """ADFVariant::InternalSolver::solve (adf.cpp:566-604) with solve_with_current_ranks (:489-542) for a
+    SinglePointMeasurementSet (positions, M x d) or a RankOneMeasurementSet (vectors[k]: M x n_k). x is
+    updated in place; returns the final relative residual norm."""
+    sp = positions is not None
+    d = x.order
+    dims = x.dims
+    M = len(values)
+    values = np.asarray(values, dtype=np.float64)
+    max_ranks = reduce_to_maximal_ranks(list(max_ranks), dims)
+    norm_meas = float(np.sqrt(np.sum(values ** 2)))   # :37-43 (sequential sum of squares)
+    state = {"it": 0, "res": np.finfo(float).max, "last": np.finfo(float).max}
+
+    def slices(C, k):   # (M, a, b): the component's matrix for each measurement
+        if sp:
+            return np.transpose(C[:, positions[:, k], :], (1, 0, 2))
+        return np.einsum("mt,atb->mab", vectors[k], C)
+
+    def value(Fm, C, Bm, k):   # Fm (M, a) . slice . Bm (M, b)
+        return np.einsum("ma,mab,mb->m", Fm, slices(C, k), Bm)
+
+    def solve_current():
+        rd1 = rd2 = rd3 = 0.0
+        Fs = {-1: np.ones((M, 1))}
+        while max_iterations == 0 or state["it"] < max_iterations:
+            x.move_core(0, keep_rank=True)
+            Bs = {d: np.ones((M, 1))}
+            for k in range(d - 1, 0, -1):   # :499-501
+                Bs[k] = np.einsum("mab,mb->ma", slices(x.cores[k], k), Bs[k + 1])
+            res = values - value(Fs[-1], x.cores[0], Bs[1], 0)
+            state["last"] = state["res"]
+            state["res"] = float(np.sqrt(np.sum(res ** 2))) / norm_meas
+            rd4, rd3, rd2 = rd3, rd2, rd1
+            rd1 = state["res"] / state["last"]
+            if state["res"] < target or rd1 * rd2 * rd3 * rd4 > min_decrease ** 4:   # :520
+                break
+            for k in range(d):   # :524-540
+                C = x.cores[k]
+                a, n, b = C.shape
+                if k > 0:
+                    res = values - value(Fs[k - 1], C, Bs[k + 1], k)
+                # projected gradient (:360-396): sum_m res_m F_m (x) e_pos / v_m (x) B_m
+                w = res[:, None, None] * Fs[k - 1][:, :, None] * Bs[k + 1][:, None, :]   # (M, a, b)
+                if sp:
+                    G = np.zeros((n, a, b))
+                    np.add.at(G, positions[:, k], w)
+                else:
+                    G = np.einsum("mt,mab->tab", vectors[k], w)
+                D = np.ascontiguousarray(np.transpose(G, (1, 0, 2)))   # (a, n, b)
+                # slicewise ||A(E(grad))||^2 (:413-465)
+                vals2 = value(Fs[k - 1], D, Bs[k + 1], k) ** 2
+                if sp:
+                    nrm = np.zeros(n)
+                    np.add.at(nrm, positions[:, k], vals2)
+                else:
+                    nrm = np.array([np.sum(vals2)])
+                # update (:468-487)
+                if sp:
+                    for j in range(n):
+                        pyr = float(np.sum(D[:, j, :] ** 2))
+                        C[:, j, :] = C[:, j, :] + (pyr / nrm[j]) * D[:, j, :]
+                else:
+                    C[...] = C + (float(np.sum(D ** 2)) / float(np.sum(nrm))) * D
+                x.cores[k] = C
+                if k + 1 < d:
+                    x.move_core(k + 1, keep_rank=True)
+                    Fs[k] = np.einsum("ma,mab->mb", Fs[k - 1], slices(x.cores[k], k))
+            state["it"] += 1
+
+    x.move_core(0)   # canonicalize_left (:582)
+    solve_current()
+    while state["res"] > target and x.ranks != max_ranks and (max_iterations == 0 or state["it"] < max_iterations):
+        x.move_core(0, keep_rank=True)   # :592-597: x + 1e-6 ||x|| rnd / ||rnd||, rnd a random rank-1 TT
+        rnd = TT.random(dims, [1] * (d - 1), rng)
+        nrnd = rnd.frob_norm()
+        diff = rnd.copy()
+        diff.cores[diff.core_position] = diff.cores[diff.core_position] * (1e-6 * x.frob_norm())
+        diff.cores[diff.core_position] = diff.cores[diff.core_position] / nrnd
+        x_new = tt_add(x, diff)
+        x_new.move_core(0)                # the sum of canonical TTs is re-canonicalised (ttNetwork.cpp:841-843)
+        x.cores, x.canonicalized, x.core_position = x_new.cores, x_new.canonicalized, x_new.core_position
+        x.round(max_ranks)
+        solve_current()
+    return state["res"]
+
+
+def tt_ones(dims: Sequence[int]) -> TT:
+    """TTNetwork::ones (ttNetwork.cpp:170-191): all-ones rank-1 components, then canonicalize_left."""
+    x = TT([np.ones((1, int(n), 1)) for n in dims])
+    x.move_core(0)
+    return x

@@ -67,6 +67,21 @@ TTTensor::TTTensor(const Tensor::DimensionTuple& _dimensions) : dimensions(_dime
     components[0][0] = 0.0;   // zero tensor, core at 0 (ttNetwork.cpp:104-105)
 }
 
+TTTensor TTTensor::ones(const std::vector<size_t>& _dimensions) {
+    XERUS_REQUIRE(std::find(_dimensions.begin(), _dimensions.end(), size_t(0)) == _dimensions.end(),
+                  "Trying to construct a TTTensor with dimension 0 is not possible.");
+    if (_dimensions.empty()) {
+        TTTensor r(size_t(0));
+        r.components[0] = Tensor::ones({});
+        return r;
+    }
+    TTTensor result(_dimensions);
+    for (size_t i = 0; i < _dimensions.size(); ++i) result.set_component(i, Tensor::ones({1, _dimensions[i], 1}));
+    result.canonicalized = false;
+    result.canonicalize_left();
+    return result;
+}
+
 TTTensor::TTTensor(const Tensor& _tensor, const double _eps, const size_t _maxRank)
     : TTTensor(_tensor, _eps, std::vector<size_t>(_tensor.degree() == 0 ? 0 : _tensor.degree() - 1, _maxRank)) {}
 

@@ -533,13 +533,14 @@ int xrs_svd_rows_vt(xrs_handle_t h, double* S, double* Vt, int* sweeps, const do
                     "xrs_svd_rows_vt: need 1 <= p <= q <= 1024 (kernel 1: p <= 512)");
         DevBuf st(h, 64);
         XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
-        jacobi_vt(h, A, int(q), false, int(p), int(q), S, Vt, int(q), st.as<int>(), 40, kernel);
-        int sts[4];
-        read_status(h, st.as<int>(), 4, sts);
+        jacobi_vt(h, A, int(q), false, int(p), int(q), S, Vt, int(q), st.as<int>(), 40, kernel, std::getenv("XRS_SVD_TIMING") != nullptr);
+        int sts[9];
+        read_status(h, st.as<int>(), 9, sts);
         *sweeps = sts[0];
         if (std::getenv("XRS_SVD_TIMING"))
-            std::fprintf(stderr, "jacobi_vt p=%zu q=%zu kernel=%d: sweeps %d, 100 MHz ticks: total %d, grid barriers %d, exchange %d\n",
-                         p, q, kernel, sts[0], sts[1], sts[2], sts[3]);
+            std::fprintf(stderr, "jacobi_vt p=%zu q=%zu kernel=%d: sweeps %d, 100 MHz ticks: total %d, grid barriers %d, exchange %d; "
+                         "thread-0 cross-round cycles: dot %d, rotation %d, update %d, barrier %d, rotations %d\n",
+                         p, q, kernel, sts[0], sts[1], sts[2], sts[3], sts[4], sts[5], sts[6], sts[7], sts[8]);
     });
 }
 

@@ -5,6 +5,7 @@
 //     A(i, j) << B(i, k) * C(k, j)
 // Everything computes on the GPU through libxerus_amd; numpy arrays are only the host interchange format.
 #include <limits>
+#include <pybind11/functional.h>
 #include <pybind11/numpy.h>
 #include <pybind11/operators.h>
 #include <pybind11/pybind11.h>
@@ -282,6 +283,7 @@ PYBIND11_MODULE(xerus, m) {
         .def_static("random_raw",
                     [](const std::vector<size_t>& _dims, const std::vector<size_t>& _ranks) { return TTTensor::random_raw(_dims, _ranks); })
         .def_static("reduce_to_maximal_ranks", &TTTensor::reduce_to_maximal_ranks)
+        .def_static("ones", &TTTensor::ones)
         .def_readonly("dimensions", &TTTensor::dimensions)
         .def_readonly("canonicalized", &TTTensor::canonicalized)
         .def_readonly("corePosition", &TTTensor::corePosition)
@@ -340,6 +342,59 @@ PYBIND11_MODULE(xerus, m) {
     m.attr("DMRG_SPD") = py::cast(ALSVariant(DMRG_SPD));
     m.attr("ASD") = py::cast(ALSVariant(ASD));
     m.attr("ASD_SPD") = py::cast(ALSVariant(ASD_SPD));
+
+    // ------------------------------------------------------------------ measurements + ADF (measurments.h, algorithms/adf.h)
+    py::class_<SinglePointMeasurementSet>(m, "SinglePointMeasurementSet")
+        .def(py::init<>())
+        .def(py::init<const SinglePointMeasurementSet&>())
+        .def_readwrite("positions", &SinglePointMeasurementSet::positions)
+        .def_readwrite("measuredValues", &SinglePointMeasurementSet::measuredValues)
+        .def_static("random", [](size_t _n, const std::vector<size_t>& _dims) { return SinglePointMeasurementSet::random(_n, _dims); })
+        .def_static("random", [](size_t _n, const Tensor& _t) { return SinglePointMeasurementSet::random(_n, _t); })
+        .def_static("random", [](size_t _n, const TTTensor& _t) { return SinglePointMeasurementSet::random(_n, _t); })
+        .def("size", &SinglePointMeasurementSet::size)
+        .def("degree", &SinglePointMeasurementSet::degree)
+        .def("frob_norm", &SinglePointMeasurementSet::frob_norm)
+        .def("add", &SinglePointMeasurementSet::add)
+        .def("sort", &SinglePointMeasurementSet::sort, py::arg("positionsOnly") = false)
+        .def("measure", py::overload_cast<const Tensor&>(&SinglePointMeasurementSet::measure))
+        .def("measure", py::overload_cast<const TTTensor&>(&SinglePointMeasurementSet::measure))
+        .def("measure", py::overload_cast<std::function<value_t(const std::vector<size_t>&)>>(&SinglePointMeasurementSet::measure))
+        .def("test", py::overload_cast<const Tensor&>(&SinglePointMeasurementSet::test, py::const_))
+        .def("test", py::overload_cast<const TTTensor&>(&SinglePointMeasurementSet::test, py::const_));
+    py::class_<RankOneMeasurementSet>(m, "RankOneMeasurementSet")
+        .def(py::init<>())
+        .def(py::init<const RankOneMeasurementSet&>())
+        .def(py::init<const SinglePointMeasurementSet&, const std::vector<size_t>&>())
+        .def_readwrite("positions", &RankOneMeasurementSet::positions)
+        .def_readwrite("measuredValues", &RankOneMeasurementSet::measuredValues)
+        .def_static("random", [](size_t _n, const std::vector<size_t>& _dims) { return RankOneMeasurementSet::random(_n, _dims); })
+        .def_static("random", [](size_t _n, const Tensor& _t) { return RankOneMeasurementSet::random(_n, _t); })
+        .def_static("random", [](size_t _n, const TTTensor& _t) { return RankOneMeasurementSet::random(_n, _t); })
+        .def("size", &RankOneMeasurementSet::size)
+        .def("degree", &RankOneMeasurementSet::degree)
+        .def("frob_norm", &RankOneMeasurementSet::frob_norm)
+        .def("add", &RankOneMeasurementSet::add)
+        .def("sort", &RankOneMeasurementSet::sort, py::arg("positionsOnly") = false)
+        .def("normalize", &RankOneMeasurementSet::normalize)
+        .def("measure", py::overload_cast<const Tensor&>(&RankOneMeasurementSet::measure))
+        .def("measure", py::overload_cast<const TTTensor&>(&RankOneMeasurementSet::measure))
+        .def("test", py::overload_cast<const Tensor&>(&RankOneMeasurementSet::test, py::const_))
+        .def("test", py::overload_cast<const TTTensor&>(&RankOneMeasurementSet::test, py::const_));
+    py::class_<ADFVariant>(m, "ADFVariant")
+        .def(py::init<size_t, double, double>(), py::arg("maxIteration"), py::arg("targetResidual"), py::arg("minimalResidualDecrease"))
+        .def_readwrite("maxIterations", &ADFVariant::maxIterations)
+        .def_readwrite("targetResidualNorm", &ADFVariant::targetResidualNorm)
+        .def_readwrite("minimalResidualNormDecrease", &ADFVariant::minimalResidualNormDecrease)
+        .def("__call__", [](const ADFVariant& _v, TTTensor& _x, const SinglePointMeasurementSet& _m) { return _v(_x, _m); })
+        .def("__call__", [](const ADFVariant& _v, TTTensor& _x, const RankOneMeasurementSet& _m) { return _v(_x, _m); })
+        .def("__call__", [](const ADFVariant& _v, TTTensor& _x, const SinglePointMeasurementSet& _m, const std::vector<size_t>& _r) {
+            return _v(_x, _m, _r);
+        })
+        .def("__call__", [](const ADFVariant& _v, TTTensor& _x, const RankOneMeasurementSet& _m, const std::vector<size_t>& _r) {
+            return _v(_x, _m, _r);
+        });
+    m.attr("ADF") = py::cast(ADFVariant(ADF));
     m.def("solve", [](const Tensor& _A, const Tensor& _B, size_t _extra) {
         Tensor X;
         solve(X, _A, _B, _extra);

@@ -55,9 +55,11 @@ void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, d
 // orthonormal rows, W = U S Vt with U S = W Vt^T. *status_dev = sweeps used, -1 if not converged in
 // max_sweeps, -2 if the block kernel's grid barrier timed out. kernel: 0 auto (p >= 32: the
 // multi-workgroup block kernel, else one workgroup with W in LDS when p (q + 1) <= 18432 doubles),
-// 1 one workgroup, 2 blocks. Enqueued only.
+// 1 one workgroup, 2 blocks. stamps (block kernel, diagnostics): status_dev[4..8] receive thread 0's
+// cycles per cross-round phase (dot, rotation, update, barrier) and its rotation count -- status_dev
+// must then hold 9 ints. Enqueued only.
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
-               int* status_dev, int max_sweeps = 40, int kernel = 0);
+               int* status_dev, int max_sweeps = 40, int kernel = 0, bool stamps = false);
 bool jacobi_vt_fits_lds(int p, int q);
 // Full SVD of the rows of W (p x q, p <= q, 32 ceil(q/32) + p <= 1024) by the block Jacobi kernel with
 // the rotations accumulated (svd.hip): W = U diag(S) Vt, U p x p orthogonal (row stride ldu), S

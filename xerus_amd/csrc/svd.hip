@@ -102,6 +102,28 @@ __device__ __forceinline__ void rotation(double a, double b, double c, double& s
     rotation(a, b, c, s, tau, tn);
 }
 
+// The same rotation with its angle from an FP32 estimate and an exactly consistent FP64 (s, tau):
+// tau = tan(theta/2) is rounded to FP32 (and then exact), s = 2 tau / (1 + tau^2) = sin(theta) to ~1 ulp,
+// so the applied transform [[1 - s tau, -s], [s, 1 - s tau]] is orthogonal to ~u whatever the angle's
+// accuracy. The angle is within ~1e-7 of the zeroing one: the pair's inner product drops by ~1e7 instead
+// of to zero, which the next sweeps absorb (the convergence test always uses fresh dot products). The
+// dependent chain is ~12 FP32 + ~8 FP64 operations instead of ~35 FP64 ones (three Newton-refined
+// FP64 reciprocals / square roots). Inputs are scaled to FP32 range by the exponent of max(|b - a|, |c|).
+// dn = the change of the first norm: a' = a + dn, b' = b - dn (a' = |x'|^2 for the applied angle).
+__device__ __forceinline__ void rotation_fast(double a, double b, double c, double& s, double& tau, double& dn) {
+    const double dd = b - a;
+    const double m = fmax(fabs(dd), fabs(c));
+    const int e = __builtin_amdgcn_frexp_exp(m);
+    const float ddf = float(__builtin_amdgcn_ldexp(dd, -e)), cf = float(__builtin_amdgcn_ldexp(c, -e));
+    const float h = __builtin_amdgcn_sqrtf(fmaf(ddf, ddf, 4.0f * cf * cf));
+    const float tf = copysignf(2.0f, ddf) * cf * __builtin_amdgcn_rcpf(fabsf(ddf) + h);   // tan(theta), |t| <= 1
+    const float tauf = tf * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_sqrtf(fmaf(tf, tf, 1.0f)));
+    tau = double(tauf);
+    s = 2.0 * tau * frcp(fma(tau, tau, 1.0));
+    const double cs = fma(-s, tau, 1.0);   // cos(theta)
+    dn = s * fma(s, dd, -2.0 * cs * c);    // sin^2 (b - a) - 2 sin cos c
+}
+
 // rows padded with zeros to E * G (no bounds checks: the padding stays zero under rotations)
 template <int G, int E>
 __device__ __forceinline__ void load_row_full(double (&x)[E], const double* __restrict__ w, int l) {
@@ -120,7 +142,7 @@ __device__ __forceinline__ void store_row_full(const double (&x)[E], double* __r
 // The register core: the lane's E elements of each row (zero beyond q, which rotations keep zero)
 // (the inner products run over the first ew elements: the rest may carry accumulated rotations)
 template <int G, int E>
-__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E) {
+__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E, bool fast = false) {
     double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -135,7 +157,12 @@ __device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], doub
     c = gsum<G>(c);
     if (!(c * c > tol2 * a * b)) return false;
     double s, tau;
-    rotation(a, b, c, s, tau);
+    if (fast) {
+        double dn;
+        rotation_fast(a, b, c, s, tau, dn);
+    } else {
+        rotation(a, b, c, s, tau);
+    }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const double xe = x[e], ye = y[e];
@@ -371,8 +398,12 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                                                                  int nb, int max_sweeps, double* __restrict__ slots,
                                                                  unsigned* __restrict__ sync, double* __restrict__ norms,
                                                                  double* __restrict__ S, double* __restrict__ Vt, int ldvt,
-                                                                 double* __restrict__ U, int ldu, int* __restrict__ status) {
+                                                                 double* __restrict__ U, int ldu, int* __restrict__ status, int flags) {
     constexpr int NT = BR * G, R2 = 2 * BR;
+    const bool stamps = (flags & 1) != 0, fast_rot = (flags & 2) != 0;
+    // diagnostics (stamps != 0, XRS_SVD_TIMING): cycles of thread 0 per cross-round phase -- dot + sum,
+    // rotation parameters, update + store, barrier wait -- and the rotation count, into status[4..8]
+    unsigned long long st_ph[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
     static_assert((BR & (BR - 1)) == 0 && BR >= 4, "BR: a power of two");
     __shared__ __attribute__((aligned(16))) double Ws[SVB_LDS];
     __shared__ int rotated, err;
@@ -426,7 +457,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                     double x[E], y[E];
                     load_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                     load_row_full<G, E>(y, Ws + (base + j) * ldw, l);
-                    if (rotate_regs<G, E>(x, y, tol2, ew)) {
+                    if (rotate_regs<G, E>(x, y, tol2, ew, fast_rot)) {
                         store_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                         store_row_full<G, E>(y, Ws + (base + j) * ldw, l);
                         if (l == 0) rotated = 1;
@@ -455,6 +486,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                 __syncthreads();
                 bool rot = false;
                 for (int sr = 0; sr < BR; ++sr) {
+                    const unsigned long long c0 = stamps ? __builtin_amdgcn_s_memtime() : 0ull;
                     const int jb = (g + sr) & (BR - 1);
                     double* wb = Wb + jb * ldw;
                     load_row_full<G, E>(y, wb, l);
@@ -464,16 +496,28 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                     for (int e = 0; e < E; ++e)
                         if (e < ew) c4[e & 3] = fma(x[e], y[e], c4[e & 3]);
                     const double c = gsum<G>((c4[0] + c4[1]) + (c4[2] + c4[3]));
-                    if (c * c > tol2 * a * b) {
-                        double sn, tau, tn;
-                        rotation(a, b, c, sn, tau, tn);
+                    const bool do_rot = c * c > tol2 * a * b;
+                    unsigned long long c1 = 0ull, c2 = 0ull;
+                    if (stamps) {
+                        c1 = __builtin_amdgcn_s_memtime() + (do_rot ? 0ull : 0ull);
+                        st_ph[0] += c1 - c0;
+                    }
+                    if (do_rot) {
+                        double sn, tau, tn = 0.0, dn = 0.0;
+                        if (fast_rot) rotation_fast(a, b, c, sn, tau, dn);
+                        else rotation(a, b, c, sn, tau, tn);
+                        if (stamps) {
+                            c2 = __builtin_amdgcn_s_memtime() + (sn != sn ? 1ull : 0ull);
+                            st_ph[1] += c2 - c1;
+                            ++st_ph[4];
+                        }
 #pragma unroll
                         for (int e = 0; e < E; ++e) {
                             const double xe = x[e], ye = y[e];
                             x[e] = xe - sn * fma(tau, xe, ye);
                             y[e] = ye + sn * fma(-tau, ye, xe);
                         }
-                        double an = fma(-tn, c, a), bnew = fma(tn, c, b);
+                        double an = fast_rot ? a + dn : fma(-tn, c, a), bnew = fast_rot ? b - dn : fma(tn, c, b);
                         if (an < 0.5 * a) {
                             an = 0.0;
 #pragma unroll
@@ -492,8 +536,14 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                         store_row_full<G, E>(y, wb, l);
                         if (l == 0) bn[jb] = bnew;
                         rot = true;
+                        if (stamps) {
+                            const unsigned long long c3 = __builtin_amdgcn_s_memtime();
+                            st_ph[2] += c3 - c2;
+                            c1 = c3;
+                        }
                     }
                     __syncthreads();
+                    if (stamps) st_ph[3] += __builtin_amdgcn_s_memtime() - c1;
                 }
                 store_row_full<G, E>(x, Ws + g * ldw, l);
                 if (rot && l == 0) rotated = 1;
@@ -564,6 +614,8 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
         status[1] = int(wall_clock64() - t_start);   // 100 MHz ticks (diagnostics)
         status[2] = int(t_bar);
         status[3] = int(t_xch);
+        if (stamps)
+            for (int i = 0; i < 5; ++i) status[4 + i] = int(st_ph[i]);
     }
 }
 
@@ -573,25 +625,37 @@ bool jacobi_vt_fits_lds(int p, int q) { return q <= 128 && size_t(p) * size_t(q 
 
 namespace {
 
+// FP32-seeded rotations (rotation_fast) in the block kernel, opt-in (XRS_SVD_FAST_ROT=1). Measured
+// (profiles/r03/svd_rotation_ab_r03k.txt): 9 % fewer cycles per cross round (1409 vs 1547; the rotation
+// parameters are not the round's bottleneck), but the inexact angles cost a sweep at 128 x 128 flat
+// (11 vs 10): no net gain, so the fully Newton-refined FP64 angle stays the default.
+bool jacobi_fast_rotations() {
+    static const bool on = [] {
+        const char* e = std::getenv("XRS_SVD_FAST_ROT");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 // block kernel launch: nb = ceil(p / BR) rounded up to even, nb / 2 one-CU workgroups (<= 32 here:
 // co-resident on any MI355X, which the grid barrier needs)
 template <int BR, int G, int E, bool ACC>
 void launch_blocks(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt, double* U,
-                   int ldu, int* status_dev, int max_sweeps) {
+                   int ldu, int* status_dev, int max_sweeps, bool stamps = false) {
     int nb = (p + BR - 1) / BR;
     nb += nb & 1;
     const int sweeps = std::min(max_sweeps, SVB_SYNC_WORDS - 1);
     DevBuf slots(h, size_t(nb) * BR * E * G * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
     XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
     hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, G, E, ACC>), dim3(nb / 2), dim3(BR * G), 0, h->stream, W, ldw, int(trans), p, q, nb, sweeps,
-                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev);
+                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev, (stamps ? 1 : 0) | (jacobi_fast_rotations() ? 2 : 0));
     check_launch("k_jacobi_vt_blocks");
 }
 
 }  // namespace
 
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
-               int* status_dev, int max_sweeps, int kernel) {
+               int* status_dev, int max_sweeps, int kernel, bool stamps) {
     XRS_REQUIRE(p >= 1 && p <= q && (p <= SV_MAXP || (q <= 2 * SVB_QMAX && kernel != 1)),
                 "jacobi_vt: need 1 <= p <= q, p <= 512 (one workgroup) or q <= 1024 (blocks)");
     XRS_REQUIRE(kernel >= 0 && kernel <= 2, "jacobi_vt: kernel is 0 (auto), 1 (one workgroup) or 2 (blocks)");
@@ -605,13 +669,13 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
     const bool blocks_ok = q <= 2 * SVB_QMAX;
     XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 1024");
     if (q > SVB_QMAX) {   // rows of up to 1024 columns: blocks of 8 rows (2 x 8 x 1024 doubles of LDS)
-        launch_blocks<8, 32, 32, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+        launch_blocks<8, 32, 32, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
     } else if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
         // register tiling E * 32 columns: the narrowest that holds q (padding costs FMAs and LDS traffic)
-        if (q <= 64) launch_blocks<16, 32, 2, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
-        else if (q <= 128) launch_blocks<16, 32, 4, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
-        else if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
-        else launch_blocks<16, 32, 16, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps);
+        if (q <= 64) launch_blocks<16, 32, 2, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
+        else if (q <= 128) launch_blocks<16, 32, 4, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
+        else if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
+        else launch_blocks<16, 32, 16, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
     } else if (jacobi_vt_fits_lds(p, q)) {
         hipLaunchKernelGGL(k_jacobi_vt_lds, dim3(1), dim3(SVL_THREADS), 0, h->stream, W, ldw, int(trans), p, q, max_sweeps, S, Vt,
                            ldvt, status_dev);
