@@ -53,6 +53,7 @@ SIGNATURES = {
     "xrs_solve": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ, _DP, _SZ]),
     "xrs_solve_least_squares": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ, _DP, _SZ]),
     "xrs_svd_rows_vt": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ, C.c_int]),
+    "xrs_sym_eig_top": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ]),
     "xrs_tt_operator_apply": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                         C.POINTER(_SZ), C.POINTER(_DP), C.c_int, C.POINTER(_DP)]),
     "xrs_tt_move_core": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ, _SZ, C.c_int]),
@@ -284,6 +285,13 @@ class Handle:
         fn = "xrs_solve_least_squares" if least_squares else "xrs_solve"
         _check(fn, getattr(self.lib, fn)(self.h, _DP(X.ptr), _DP(A.ptr), m, n, _DP(B.ptr), p))
         return X
+
+    def sym_eig_top(self, A: "DeviceArray", kk: int):
+        """(lam, Ut, status): the kk largest eigenpairs of the symmetric A (n <= 128), xrs_sym_eig_top."""
+        n = A.shape[0]
+        lam, Ut, st = self.empty((kk,)), self.empty((kk, n)), C.c_int()
+        _check("xrs_sym_eig_top", self.lib.xrs_sym_eig_top(self.h, _DP(lam.ptr), _DP(Ut.ptr), C.byref(st), _DP(A.ptr), n, kk))
+        return lam, Ut, st.value
 
     def svd_rows_vt(self, A: "DeviceArray", kernel: int = 0):
         """(S, Vt, sweeps) of the rows of A (p <= q <= 512) by one-sided Jacobi (xrs_svd_rows_vt)."""

@@ -526,6 +526,18 @@ int xrs_svd(xrs_handle_t h, double* U, double* S, double* Vt, const double* A, s
     });
 }
 
+int xrs_sym_eig_top(xrs_handle_t h, double* lam, double* Ut, int* status, const double* A, size_t n, size_t kk) {
+    return guarded([&] {
+        XRS_REQUIRE(h && lam && Ut && status && A, "null argument");
+        XRS_REQUIRE(sym_eig_top_fits(int(n), int(kk)), "xrs_sym_eig_top: need 2 <= n <= 128 and 1 <= kk <= n");
+        fence_readers(h);
+        DevBuf st(h, 64);
+        XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
+        sym_eig_top(h, A, int(n), int(n), int(kk), lam, nullptr, Ut, int(n), st.as<int>());
+        read_status(h, st.as<int>(), 1, status);
+    });
+}
+
 int xrs_svd_rows_vt(xrs_handle_t h, double* S, double* Vt, int* sweeps, const double* A, size_t p, size_t q, int kernel) {
     return guarded([&] {
         XRS_REQUIRE(h && S && Vt && A && sweeps, "null argument");

@@ -1,0 +1,470 @@
+// Top-kk eigenpairs of a symmetric n x n matrix (n <= 128) for the certified truncating round: the
+// reference computes the edge's singular vectors with dgesdd (tensor.cpp:1424-1489); where the round has
+// certified the edge Gram P = B B^T to be well conditioned and the kept rank kk is fixed in advance
+// (tt_trunc.hip round_truncate), the kept left singular vectors of B are the eigenvectors of P's kk
+// largest eigenvalues. Three launches, LAPACK's dsytrd / dstebz / dstein / dormtr structure:
+//   1. k_sytrd: Householder tridiagonalisation A = Q T Q^T in ONE workgroup, the matrix register-resident
+//      (1024 threads on a 32 x 32 grid, element (i, k) on thread (i mod 32, k mod 32): the shrinking trailing
+//      block stays spread over every thread). Per column: the reflector from one wave, the symmetric
+//      matrix-vector product with in-half-wave reductions, the rank-2 update in registers -- 4 barriers.
+//   2. k_stebz_stein: one wave per wanted eigenvalue (kk workgroups in parallel): Sturm-count
+//      multisection on 64 points per round (~9 rounds to full precision), then inverse iteration with the
+//      partially pivoted LU of T - lambda I (dgttrf / dgttrs), three solves from a fixed start vector.
+//   3. k_ormtr: the eigenvectors back to A's coordinates, u = H_0 ... H_{n-2} z, 16 vectors per workgroup
+//      (16 lanes each), the reflectors read from L2.
+// Inverse iteration is accurate for eigenvalues separated relative to ||T|| (the certified rounds' random
+// spectra); a cluster would give non-orthogonal vectors, which the round's final orthonormality check
+// rejects (then the reference's algorithm runs).
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "smallla.hpp"
+
+namespace xrs {
+
+namespace {
+
+constexpr int SY_MAX = 256;
+
+// Cross-lane sums without the LDS crossbar (a __shfl_xor of a double is two ds_bpermute round trips, the
+// bulk of a column step when chained): DPP row rotations within 16 lanes, v_permlane16_swap across the
+// two rows of a 32-lane half, one shuffle across the halves.
+template <int CTRL>
+__device__ __forceinline__ double dpp(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double xor16(double v) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return (threadIdx.x & 16) ? __hiloint2double(hi[0], lo[0]) : __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double sum16(double v) {   // every lane of the 16-lane row gets the row's sum
+    v += dpp<0x128>(v);
+    v += dpp<0x124>(v);
+    v += dpp<0x122>(v);
+    v += dpp<0x121>(v);
+    return v;
+}
+__device__ __forceinline__ double sum32(double v) { v = sum16(v); return v + xor16(v); }
+__device__ __forceinline__ double sum64(double v) { v = sum32(v); return v + __shfl_xor(v, 32, 64); }
+
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
+// stores (__syncthreads' release fence would drain the per-column stores of the reflectors, d, e and tau
+// to memory at every barrier of the column loop)
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__device__ __forceinline__ double rcp2(double x) {   // 1/x to ~1 ulp (hardware estimate + 2 Newton steps)
+    double r = __builtin_amdgcn_rcp(x);
+    double t = fma(-x, r, 1.0);
+    r = fma(r, t, r);
+    t = fma(-x, r, 1.0);
+    return fma(r, t, r);
+}
+
+// LAPACK dsytd2 (lower) on the register grid. V: row j = Householder vector v_j (v_j[i] = 0 for i <= j,
+// v_j[j + 1] = 1); d (n), e (n - 1), tau (n - 1). A is read from its lower triangle.
+template <int NB>
+__global__ void __launch_bounds__(1024) k_sytrd(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
+                                                double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V,
+                                                unsigned long long* __restrict__ stamps) {
+    // diagnostics (stamps != null): threads 0 and 64 record s_memtime at 6 points of every column step
+#define SYTRD_STAMP(p)                                                                                  \
+    do {                                                                                                \
+        if (stamps && (threadIdx.x == 0 || threadIdx.x == 64) && j < 64)                                 \
+            stamps[(threadIdx.x == 0 ? 0 : 384) + 6 * j + (p)] = __builtin_amdgcn_s_memtime();           \
+    } while (0)
+    __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX];
+    __shared__ double sh_tau;
+    const int t = threadIdx.x, tr = t >> 5, tc = t & 31, lane = t & 63, wave = t >> 6;
+    double a[NB][NB];
+#pragma unroll
+    for (int ia = 0; ia < NB; ++ia)
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+            const int i = tr + 32 * ia, k = tc + 32 * ib;
+            a[ia][ib] = (i < n && k < n) ? (i >= k ? A[size_t(i) * lda + k] : A[size_t(k) * lda + i]) : 0.0;
+        }
+    // column j of the current matrix to LDS (xs) and its diagonal entry to d, by the column's owners
+    auto publish_column = [&](int j) {
+        if (tc == (j & 31)) {
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) {
+                const int i = tr + 32 * ia;
+#pragma unroll
+                for (int ib = 0; ib < NB; ++ib)
+                    if (ib == (j >> 5)) {
+                        if (i > j && i < n) xs[i] = a[ia][ib];
+                        if (i == j) d[j] = a[ia][ib];
+                    }
+            }
+        }
+    };
+    publish_column(0);
+    for (int j = 0; j + 2 < n; ++j) {
+        SYTRD_STAMP(0);
+        lds_barrier();
+        SYTRD_STAMP(1);
+        // (b) reflector (dlarfg): beta = -sign(alpha) ||(alpha, x)||, tau = (beta - alpha) / beta,
+        //     v = (1, x / (alpha - beta))
+        if (wave == 0) {
+            constexpr int E = NB / 2;   // entries per lane of the 32 NB = 64 E padded indices
+            double x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = xs[lane + 64 * q];
+            const double alpha = xs[j + 1];
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int i = lane + 64 * q;
+                if (i >= j + 2 && i < n) s = fma(x[q], x[q], s);
+            }
+            s = sum64(s);
+            double tv = 0.0, beta = alpha, scal = 0.0;
+            if (s > 0.0) {
+                beta = -copysign(sqrt(fma(alpha, alpha, s)), alpha);
+                tv = (beta - alpha) * rcp2(beta);
+                scal = rcp2(alpha - beta);
+            }
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int i = lane + 64 * q;
+                const double v = (i <= j || i >= n) ? 0.0 : (i == j + 1 ? 1.0 : x[q] * scal);
+                vs[i] = v;
+                if (i < n) V[size_t(j) * n + i] = v;
+            }
+            if (lane == 0) {
+                sh_tau = tv;
+                e[j] = beta;
+                tau[j] = tv;
+            }
+        }
+        SYTRD_STAMP(2);
+        lds_barrier();
+        SYTRD_STAMP(3);
+        const double tj = sh_tau;
+        if (tj == 0.0) {   // H_j = I (uniform): the next column is already final
+            publish_column(j + 1);
+            continue;
+        }
+        // (c) p = tau A v on the trailing block: row partials (NB independent chains), reduced over the 32
+        //     column threads of a row level by level across the rows (ILP in the DPP chain)
+        {
+            double part[NB], vcol[NB];
+#pragma unroll
+            for (int ib = 0; ib < NB; ++ib) vcol[ib] = vs[tc + 32 * ib];
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) {
+                part[ia] = 0.0;
+#pragma unroll
+                for (int ib = 0; ib < NB; ++ib) part[ia] = fma(a[ia][ib], vcol[ib], part[ia]);
+            }
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x128>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x124>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x122>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x121>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += xor16(part[ia]);
+            if (tc == 0) {
+#pragma unroll
+                for (int ia = 0; ia < NB; ++ia) {
+                    const int i = tr + 32 * ia;
+                    ps[i] = (i > j && i < n) ? tj * part[ia] : 0.0;
+                }
+            }
+        }
+        if (t < SY_MAX && t >= 32 * NB) ps[t] = 0.0;
+        SYTRD_STAMP(4);
+        lds_barrier();
+        SYTRD_STAMP(5);
+        // (d) every wave forms K = -(tau / 2) (p . v) itself (no extra barrier), w = p + K v on the fly;
+        //     the update's operands are read before the reduction so their LDS latency overlaps it
+        double vr[NB], pr[NB], vc[NB], pc[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            vr[q] = vs[tr + 32 * q];
+            pr[q] = ps[tr + 32 * q];
+            vc[q] = vs[tc + 32 * q];
+            pc[q] = ps[tc + 32 * q];
+        }
+        double sk = 0.0;
+#pragma unroll
+        for (int q = 0; q < NB / 2; ++q) sk = fma(ps[lane + 64 * q], vs[lane + 64 * q], sk);
+        const double K = -0.5 * tj * sum64(sk);
+        // (e) A -= v w^T + w v^T (v, w vanish at indices <= j: finished rows and columns stay untouched)
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+            const double wc = fma(K, vc[ib], pc[ib]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) a[ia][ib] = fma(-vr[ia], wc, fma(-fma(K, vr[ia], pr[ia]), vc[ib], a[ia][ib]));
+        }
+        publish_column(j + 1);
+    }
+#undef SYTRD_STAMP
+    // the last 2 x 2 block: d[n-2], d[n-1], e[n-2] (tau = 0, H = I)
+#pragma unroll
+    for (int ia = 0; ia < NB; ++ia)
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+            const int i = tr + 32 * ia, k = tc + 32 * ib;
+            if (n >= 2 && i == n - 2 && k == n - 2) d[n - 2] = a[ia][ib];
+            if (n >= 1 && i == n - 1 && k == n - 1) d[n - 1] = a[ia][ib];
+            if (n >= 2 && i == n - 1 && k == n - 2) {
+                e[n - 2] = a[ia][ib];
+                tau[n - 2] = 0.0;
+                for (int q = 0; q < n; ++q) V[size_t(n - 2) * n + q] = 0.0;
+            }
+        }
+}
+
+// one 64-lane workgroup per wanted eigenvalue: block q -> the q-th largest (ascending index n - 1 - q).
+// Zt (kk x ldz): row q = the eigenvector of T (normalised); lam[q]. status[0] <- -1 if a multisection
+// did not reach full precision.
+__global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
+                                                     double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status) {
+    __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX];
+    __shared__ double ld[SY_MAX], ldl[SY_MAX], ldu[SY_MAX], ldu2[SY_MAX], lb[SY_MAX];
+    __shared__ int lpiv[SY_MAX];
+    const int lane = threadIdx.x, q = blockIdx.x, m = n - 1 - q;
+    double gl = 1e300, gu = -1e300, emax2 = 0.0, amax = 0.0;
+    for (int i = lane; i < n; i += 64) {
+        const double di = d[i], ei = i + 1 < n ? e[i] : 0.0, em = i > 0 ? e[i - 1] : 0.0;
+        sd[i] = di;
+        se[i] = ei;
+        se2[i] = ei * ei;
+        const double r = fabs(ei) + fabs(em);
+        gl = fmin(gl, di - r);
+        gu = fmax(gu, di + r);
+        emax2 = fmax(emax2, ei * ei);
+        amax = fmax(amax, fabs(di) + r);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        gl = fmin(gl, __shfl_xor(gl, o, 64));
+        gu = fmax(gu, __shfl_xor(gu, o, 64));
+        emax2 = fmax(emax2, __shfl_xor(emax2, o, 64));
+        amax = fmax(amax, __shfl_xor(amax, o, 64));
+    }
+    __syncthreads();
+    const double pivmin = 1e-290 * fmax(1.0, emax2);
+    const double span = fmax(gu - gl, 1e-300);
+    double lo = gl - 2.2e-16 * span - pivmin, hi = gu + 2.2e-16 * span + pivmin;
+    // multisection: lane l counts the eigenvalues below lo + (hi - lo) (l + 1) / 65
+    int rounds = 0;
+    bool done = false;
+    for (; rounds < 16 && !done; ++rounds) {
+        const double x = lo + (hi - lo) * double(lane + 1) * (1.0 / 65.0);
+        double qv = sd[0] - x;
+        if (fabs(qv) < pivmin) qv = -pivmin;
+        int c = qv < 0.0;
+        for (int i = 1; i < n; ++i) {
+            qv = (sd[i] - x) - se2[i - 1] * rcp2(qv);
+            if (fabs(qv) < pivmin) qv = -pivmin;
+            c += qv < 0.0;
+        }
+        double nlo = c <= m ? x : -1e300, nhi = c >= m + 1 ? x : 1e300;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            nlo = fmax(nlo, __shfl_xor(nlo, o, 64));
+            nhi = fmin(nhi, __shfl_xor(nhi, o, 64));
+        }
+        if (nlo > lo) lo = nlo;
+        if (nhi < hi) hi = nhi;
+        // absolute accuracy u ||T|| (dstebz's default abstol): all a backward-stable reduction delivers
+        done = (hi - lo) <= 2.2204460492503131e-16 * (2.0 * fmax(fabs(lo), fabs(hi)) + 4.0 * span) + 2.0 * pivmin;
+    }
+    const double lmb = 0.5 * (lo + hi);
+    __shared__ double ild[SY_MAX];   // inverse pivots of U
+    if (lane == 0) {
+        lam[q] = lmb;
+        if (!done) atomicMin(status, -1);
+        // inverse iteration: T - lambda I = P L U (dgttrf, row interchanges where the subdiagonal entry is
+        // larger), tiny pivots replaced by u ||T|| (dlagtf's perturbation)
+        for (int i = 0; i < n; ++i) {
+            ld[i] = sd[i] - lmb;
+            ldl[i] = i + 1 < n ? se[i] : 0.0;
+            ldu[i] = i + 1 < n ? se[i] : 0.0;
+            ldu2[i] = 0.0;
+            lpiv[i] = i;
+        }
+        for (int i = 0; i + 1 < n; ++i) {
+            if (fabs(ld[i]) >= fabs(ldl[i])) {
+                if (ld[i] != 0.0) {
+                    const double f = ldl[i] * rcp2(ld[i]);
+                    ldl[i] = f;
+                    ld[i + 1] -= f * ldu[i];
+                }
+            } else {
+                const double f = ld[i] * rcp2(ldl[i]);
+                ld[i] = ldl[i];
+                ldl[i] = f;
+                const double tmp = ldu[i];
+                ldu[i] = ld[i + 1];
+                ld[i + 1] = tmp - f * ld[i + 1];
+                if (i + 2 < n) {
+                    ldu2[i] = ldu[i + 1];
+                    ldu[i + 1] = -f * ldu[i + 1];
+                }
+                lpiv[i] = i + 1;
+            }
+        }
+    }
+    __syncthreads();
+    {
+        const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
+        for (int i = lane; i < n; i += 64) {
+            double p = ld[i];
+            if (fabs(p) < tiny) p = copysign(tiny, p == 0.0 ? 1.0 : p);
+            ild[i] = rcp2(p);
+            lb[i] = 1.0 + double((i * 37 + q * 11) % 17) * (1.0 / 17.0);
+        }
+    }
+    __syncthreads();
+    for (int it = 0; it < 3; ++it) {
+        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in registers)
+            double cur = lb[0];
+            for (int i = 0; i + 1 < n; ++i) {
+                const double nxt = lb[i + 1], f = ldl[i];
+                if (lpiv[i] == i) {
+                    lb[i] = cur;
+                    cur = fma(-f, cur, nxt);
+                } else {
+                    lb[i] = nxt;
+                    cur = fma(-f, nxt, cur);
+                }
+            }
+            double x1 = cur * ild[n - 1], x2 = 0.0;
+            lb[n - 1] = x1;
+            for (int i = n - 2; i >= 0; --i) {
+                const double x0 = (lb[i] - ldu[i] * x1 - ldu2[i] * x2) * ild[i];
+                lb[i] = x0;
+                x2 = x1;
+                x1 = x0;
+            }
+        }
+        __syncthreads();
+        // normalise (scaled 2-norm over the wave)
+        double mx = 0.0;
+        for (int i = lane; i < n; i += 64) mx = fmax(mx, fabs(lb[i]));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, 64));
+        const double inv_mx = mx > 0.0 ? 1.0 / mx : 1.0;
+        double ss = 0.0;
+        for (int i = lane; i < n; i += 64) {
+            const double v = lb[i] * inv_mx;
+            ss = fma(v, v, ss);
+        }
+        ss = sum64(ss);
+        const double sc = inv_mx / sqrt(ss);
+        __syncthreads();
+        for (int i = lane; i < n; i += 64) lb[i] *= sc;
+        __syncthreads();
+    }
+    for (int i = lane; i < n; i += 64) Zt[size_t(q) * ldz + i] = lb[i];
+}
+
+// u = H_0 H_1 ... H_{n-2} z for every row z of Zt (in place): 16 vectors per 256-thread workgroup, 16 lanes
+// per vector holding n / 16 entries each
+__global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, const double* __restrict__ tau, int n, int kk,
+                                               double* __restrict__ Zt, int ldz) {
+    // every reflector and tau staged in LDS once (n <= 128: 128 KB), read per application by 16 lanes each
+    __shared__ double sv[128 * 128 + 128];
+    for (int e = threadIdx.x; e < (n - 1) * n; e += 256) sv[e] = V[e];
+    for (int e = threadIdx.x; e < n; e += 256) sv[128 * 128 + e] = e + 1 < n ? tau[e] : 0.0;
+    __syncthreads();
+    const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
+    const int q = blockIdx.x * 16 + g;
+    const bool live = q < kk;
+    double z[128 / 16];
+#pragma unroll
+    for (int s = 0; s < 128 / 16; ++s) {
+        const int i = l + 16 * s;
+        z[s] = (live && i < n) ? Zt[size_t(q) * ldz + i] : 0.0;
+    }
+    for (int j = n - 2; j >= 0; --j) {
+        const double tj = sv[128 * 128 + j];
+        if (tj == 0.0) continue;
+        const double* v = sv + size_t(j) * n;
+        double vv[128 / 16];
+        double dot = 0.0;
+#pragma unroll
+        for (int s = 0; s < 128 / 16; ++s) {
+            const int i = l + 16 * s;
+            vv[s] = i < n ? v[i] : 0.0;
+            dot = fma(vv[s], z[s], dot);
+        }
+        const double f = tj * sum16(dot);
+#pragma unroll
+        for (int s = 0; s < 128 / 16; ++s) z[s] = fma(-f, vv[s], z[s]);
+    }
+    if (live) {
+#pragma unroll
+        for (int s = 0; s < 128 / 16; ++s) {
+            const int i = l + 16 * s;
+            if (i < n) Zt[size_t(q) * ldz + i] = z[s];
+        }
+    }
+}
+
+__global__ void k_sqrt_lam(const double* __restrict__ lam, int kk, double* __restrict__ S) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < kk) S[i] = sqrt(fmax(lam[i], 0.0));
+}
+
+}  // namespace
+
+// (n <= 128: the register grid holds 16 doubles per thread; 256 would need 64, beyond the 128 VGPRs of a
+// 1024-thread workgroup)
+bool sym_eig_top_fits(int n, int kk) { return n >= 2 && n <= 128 && kk >= 1 && kk <= n; }
+
+void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status) {
+    XRS_REQUIRE(sym_eig_top_fits(n, kk), "sym_eig_top: need 2 <= n <= 256 and 1 <= kk <= n");
+    DevBuf dbuf(h, size_t(n) * 8), ebuf(h, size_t(n) * 8), tbuf(h, size_t(n) * 8), V(h, size_t(n) * n * 8), lbuf(h, size_t(kk) * 8);
+    double* lm = lam ? lam : lbuf.d();
+    KernelTimer timer(h, XRS_KFAM_SVD, 4.0 / 3.0 * double(n) * n * n + 4.0 * double(n) * n * kk, 8.0 * double(n) * n * 2);
+    static const bool want_stamps = std::getenv("XRS_SYEV_STAMPS") != nullptr;
+    DevBuf sb(h, want_stamps ? 768 * 8 : 0);
+    unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
+    if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 768 * 8, h->stream));
+    if (n <= 64) hipLaunchKernelGGL((k_sytrd<2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
+    else hipLaunchKernelGGL((k_sytrd<4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
+    check_launch("k_sytrd");
+    hipLaunchKernelGGL(k_stebz_stein, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
+    check_launch("k_stebz_stein");
+    hipLaunchKernelGGL(k_ormtr, dim3((kk + 15) / 16), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    check_launch("k_ormtr");
+    if (stp) {   // per-phase cycles of the first steps: (b)-wait, reflector, wait, symv, wait, update (+ column)
+        std::vector<unsigned long long> hst(768);
+        XRS_HIP(hipMemcpyAsync(hst.data(), stp, 768 * 8, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        for (int w = 0; w < 2; ++w) {
+            double ph[6] = {0, 0, 0, 0, 0, 0};
+            int steps = 0;
+            for (int j = 0; j + 1 < std::min(n - 2, 64); ++j) {
+                const unsigned long long* a = hst.data() + 384 * w + 6 * j;
+                const unsigned long long nxt = a[6];
+                if (!a[0] || !nxt) continue;
+                ph[0] += double(a[1] - a[0]); ph[1] += double(a[2] - a[1]); ph[2] += double(a[3] - a[2]);
+                ph[3] += double(a[4] - a[3]); ph[4] += double(a[5] - a[4]); ph[5] += double(nxt - a[5]);
+                ++steps;
+            }
+            std::fprintf(stderr, "k_sytrd n=%d thread %d: mean cycles per step over %d: barrier1 %.0f reflector %.0f barrier2 %.0f symv %.0f barrier3 %.0f update %.0f\n",
+                         n, w ? 64 : 0, steps, ph[0] / steps, ph[1] / steps, ph[2] / steps, ph[3] / steps, ph[4] / steps, ph[5] / steps);
+        }
+    }
+    if (S) {
+        hipLaunchKernelGGL(k_sqrt_lam, dim3((kk + 255) / 256), dim3(256), 0, h->stream, lm, kk, S);
+        check_launch("k_sqrt_lam");
+    }
+}
+
+}  // namespace xrs

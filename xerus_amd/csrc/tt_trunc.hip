@@ -335,17 +335,24 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         if (wide) gemm_sym(h, P, g, 1.0, B, N, false, N, B, N, true);
         else gemm_sym(h, P, g, 1.0, B, N, true, r, B, N, false);
         if (wide) t.reduce(P, g * g);   // sharded: sum over the mode slices
-        double* L = sw.buf(g * g);
-        double* Z = g > 256 ? sw.buf(g * g) : nullptr;   // (factor_big always builds L^{-1})
-        const std::vector<CholJob> cj{{P, int(g), L, Z}, {P, int(g), nullptr, nullptr}};
+        // the kept subspace: P's kk dominant eigenvectors. The certificate chol(P - tau tr(P) I) bounds
+        // kappa(P) <= 4 / tau, so P's eigenvectors are accurate to u kappa-free relative gaps and no eps cut
+        // can fire (kk is known): up to 256 by the tridiagonal eigensolver (syev.hip, ~10x faster than the
+        // Jacobi sweeps), above it (or XRS_TRUNC_JACOBI=1) by one-sided Jacobi on the rows of L^T, i.e. on
+        // the columns of the Cholesky factor (Drmac-Veselic: far fewer sweeps than the factor's rows)
+        static const bool force_jacobi = std::getenv("XRS_TRUNC_JACOBI") != nullptr;
+        const bool use_eig = !force_jacobi && sym_eig_top_fits(int(g), int(kk));
+        double* L = use_eig ? nullptr : sw.buf(g * g);
+        double* Z = (!use_eig && g > 256) ? sw.buf(g * g) : nullptr;   // (factor_big always builds L^{-1})
+        std::vector<CholJob> cj{{P, int(g), nullptr, nullptr}};
+        if (!use_eig) cj.insert(cj.begin(), CholJob{P, int(g), L, Z});
         chol_jobs(sw, cj, status + nst);
         nst += chol_status_count(cj);
-        // one-sided Jacobi on the rows of L^T, i.e. on the columns of the Cholesky factor (Drmac-Veselic:
-        // the triangular factor's transpose converges in far fewer sweeps than the factor itself)
         double* S = sw.buf(g);
         double* Vt = wide ? sw.buf(g * g) : sw.core(g * g);
         int* js = status + kJacobiSlot + int(jst.size());
-        jacobi_vt(h, L, int(g), true, int(g), int(g), S, Vt, int(g), js);
+        if (use_eig) sym_eig_top(h, P, int(g), int(g), int(kk), nullptr, S, Vt, int(g), js);
+        else jacobi_vt(h, L, int(g), true, int(g), int(g), S, Vt, int(g), js);
         jst.push_back(js);
         double* Tk = sw.buf(r * kk);
         double* newk;
