@@ -77,7 +77,9 @@ def random_cores(xe, dims, ranks, seed):
 
 def load_traffic():
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC pass of this bench (or None)."""
-    p = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
+    p = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
+    if not os.path.exists(p):
+        p = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
