@@ -142,7 +142,7 @@ int xrs_solve_least_squares(xrs_handle_t handle, double* X, const double* A, siz
  *  kernel: 0 auto, 1 one workgroup, 2 multi-workgroup blocks (p > 16). *sweeps (host): Jacobi
  *  sweeps used, -1 not converged, -2 grid-barrier timeout. Synchronises. */
 int xrs_svd_rows_vt(xrs_handle_t handle, double* S, double* Vt, int* sweeps, const double* A, size_t p, size_t q, int kernel);
-/** Eigenpairs of the kk largest eigenvalues of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 128,
+/** Eigenpairs of the kk largest eigenvalues of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 256,
  *  1 <= kk <= n): the certified truncating round's replacement of the per-edge SVD when the edge Gram is
  *  certified well conditioned (no reference counterpart: the reference always runs dgesdd, tensor.cpp:1424-1489).
  *  Householder tridiagonalisation, multisection + inverse iteration, back-transformation. lam: kk descending;

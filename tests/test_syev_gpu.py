@@ -1,5 +1,5 @@
 """The certified truncating round's eigensolver (xrs_sym_eig_top, csrc/syev.hip) vs LAPACK dsyevd (numpy):
-the kk largest eigenpairs of symmetric matrices up to 128, with flat, graded and clustered-free spectra.
+the kk largest eigenpairs of symmetric matrices up to 256, with flat, graded and clustered-free spectra.
 Bars: eigenvalues to 1e-13 ||A||, eigenvectors orthonormal to 1e-12 and residual ||A u - lam u|| to 1e-12 ||A||
 (the round additionally checks the orthonormality of every new core and falls back on failure)."""
 import numpy as np
@@ -15,7 +15,8 @@ def _spd(n, spectrum, seed):
 
 
 @pytest.mark.parametrize("n,kk,kind", [(2, 1, "flat"), (5, 5, "flat"), (33, 7, "flat"), (64, 64, "flat"), (64, 32, "graded"),
-                                       (100, 50, "flat"), (128, 64, "flat"), (128, 48, "graded"), (128, 20, "wishart")])
+                                       (100, 50, "flat"), (128, 64, "flat"), (128, 48, "graded"), (128, 20, "wishart"),
+                                       (129, 60, "flat"), (200, 100, "wishart"), (256, 128, "wishart"), (256, 256, "flat")])
 def test_sym_eig_top(handle, n, kk, kind):
     rng = np.random.default_rng(n * 7 + kk)
     if kind == "flat":

@@ -25,8 +25,23 @@ cores = bench.random_cores(xe, [n] * d, ranks, bench.SEED + 11)
 if graded:
     for k in range(d - 1):
         cores[k] = cores[k] * (float(graded) ** np.arange(cores[k].shape[2]))[None, None, :]
+if os.environ.get("SUM"):   # (x + y) with y a second random TT of the same ranks: block-diagonal cores, rank 2r
+    c2 = bench.random_cores(xe, [n] * d, ranks, bench.SEED + 12)
+    sc = []
+    for k in range(d):
+        X, Y = cores[k], c2[k]
+        if k == 0:
+            sc.append(np.concatenate([X, Y], axis=2))
+        elif k == d - 1:
+            sc.append(np.concatenate([X, Y], axis=0))
+        else:
+            Z = np.zeros((X.shape[0] + Y.shape[0], n, X.shape[2] + Y.shape[2]))
+            Z[:X.shape[0], :, :X.shape[2]] = X
+            Z[X.shape[0]:, :, X.shape[2]:] = Y
+            sc.append(Z)
+    cores = sc
 x = capi.TTDevice.from_cores(h, cores)
-if not graded:
+if not graded and not os.environ.get("SUM"):
     x.move_core(0)
 for i in range(reps):
     c = x.clone()

@@ -64,12 +64,12 @@ bool jacobi_vt_fits_lds(int p, int q);
 // Full SVD of the rows of W (p x q, p <= q, 32 ceil(q/32) + p <= 1024) by the block Jacobi kernel with
 // the rotations accumulated (svd.hip): W = U diag(S) Vt, U p x p orthogonal (row stride ldu), S
 // descending, Vt p x q (orthonormal rows for S > 0). Status as jacobi_vt. Enqueued only.
-// Eigenpairs of the kk largest eigenvalues of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 128):
+// Eigenpairs of the kk largest eigenvalues of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 256):
 // Householder tridiagonalisation (one workgroup, register-resident), multisection + inverse iteration per
 // eigenvalue, back-transformation (syev.hip). lam (kk, optional) descending, S = sqrt(max(lam, 0))
 // (optional), Ut rows = the eigenvectors (kk x n, row stride ldu). *status_dev set to -1 if a
 // multisection did not converge (left untouched otherwise). Enqueued only.
-bool sym_eig_top_fits(int n, int kk);
+bool sym_eig_top_fits(int n, int kk);   // the truncating round's policy (n <= 128 unless XRS_SYEV_MAX)
 void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status_dev);
 bool jacobi_usv_fits(int p, int q);
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,

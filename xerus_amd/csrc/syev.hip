@@ -1,4 +1,4 @@
-// Top-kk eigenpairs of a symmetric n x n matrix (n <= 128) for the certified truncating round: the
+// Top-kk eigenpairs of a symmetric n x n matrix (n <= 256) for the certified truncating round: the
 // reference computes the edge's singular vectors with dgesdd (tensor.cpp:1424-1489); where the round has
 // certified the edge Gram P = B B^T to be well conditioned and the kept rank kk is fixed in advance
 // (tt_trunc.hip round_truncate), the kept left singular vectors of B are the eigenvectors of P's kk
@@ -15,6 +15,7 @@
 // Inverse iteration is accurate for eigenvalues separated relative to ||T|| (the certified rounds' random
 // spectra); a cluster would give non-orthogonal vectors, which the round's final orthonormality check
 // rejects (then the reference's algorithm runs).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -67,10 +68,12 @@ __device__ __forceinline__ double rcp2(double x) {   // 1/x to ~1 ulp (hardware 
     return fma(r, t, r);
 }
 
-// LAPACK dsytd2 (lower) on the register grid. V: row j = Householder vector v_j (v_j[i] = 0 for i <= j,
+// LAPACK dsytd2 (lower) on the register grid (element (i, k) on thread (i mod GRID, k mod GRID)). V: row j = Householder vector v_j (v_j[i] = 0 for i <= j,
 // v_j[j + 1] = 1); d (n), e (n - 1), tau (n - 1). A is read from its lower triangle.
-template <int NB>
-__global__ void __launch_bounds__(1024) k_sytrd(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
+// GRID x GRID threads (GRID = 32: 16 waves; GRID = 16: 4 waves, one per SIMD, NB x NB = 64 elements per
+// thread at n = 128 -- fewer waves to wait for at every barrier and no SIMD shared between waves)
+template <int GRID, int NB>
+__global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
                                                 double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V,
                                                 unsigned long long* __restrict__ stamps) {
     // diagnostics (stamps != null): threads 0 and 64 record s_memtime at 6 points of every column step
@@ -81,24 +84,25 @@ __global__ void __launch_bounds__(1024) k_sytrd(const double* __restrict__ A, in
     } while (0)
     __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX];
     __shared__ double sh_tau;
-    const int t = threadIdx.x, tr = t >> 5, tc = t & 31, lane = t & 63, wave = t >> 6;
+    const int t = threadIdx.x, tr = t / GRID, tc = t % GRID, lane = t & 63, wave = t >> 6;
+    constexpr int NP = GRID * NB;   // padded order
     double a[NB][NB];
 #pragma unroll
     for (int ia = 0; ia < NB; ++ia)
 #pragma unroll
         for (int ib = 0; ib < NB; ++ib) {
-            const int i = tr + 32 * ia, k = tc + 32 * ib;
+            const int i = tr + GRID * ia, k = tc + GRID * ib;
             a[ia][ib] = (i < n && k < n) ? (i >= k ? A[size_t(i) * lda + k] : A[size_t(k) * lda + i]) : 0.0;
         }
     // column j of the current matrix to LDS (xs) and its diagonal entry to d, by the column's owners
     auto publish_column = [&](int j) {
-        if (tc == (j & 31)) {
+        if (tc == (j % GRID)) {
 #pragma unroll
             for (int ia = 0; ia < NB; ++ia) {
-                const int i = tr + 32 * ia;
+                const int i = tr + GRID * ia;
 #pragma unroll
                 for (int ib = 0; ib < NB; ++ib)
-                    if (ib == (j >> 5)) {
+                    if (ib == (j / GRID)) {
                         if (i > j && i < n) xs[i] = a[ia][ib];
                         if (i == j) d[j] = a[ia][ib];
                     }
@@ -113,7 +117,162 @@ __global__ void __launch_bounds__(1024) k_sytrd(const double* __restrict__ A, in
         // (b) reflector (dlarfg): beta = -sign(alpha) ||(alpha, x)||, tau = (beta - alpha) / beta,
         //     v = (1, x / (alpha - beta))
         if (wave == 0) {
-            constexpr int E = NB / 2;   // entries per lane of the 32 NB = 64 E padded indices
+            constexpr int E = NP >= 64 ? NP / 64 : 1;   // entries per lane of the NP padded indices
+            double x[E];
+#pragma unroll
+            for (int q = 0; q < E; ++q) x[q] = (lane + 64 * q < NP) ? xs[lane + 64 * q] : 0.0;
+            const double alpha = xs[j + 1];
+            double s = 0.0;
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int i = lane + 64 * q;
+                if (i >= j + 2 && i < n) s = fma(x[q], x[q], s);
+            }
+            s = sum64(s);
+            double tv = 0.0, beta = alpha, scal = 0.0;
+            if (s > 0.0) {
+                beta = -copysign(sqrt(fma(alpha, alpha, s)), alpha);
+                tv = (beta - alpha) * rcp2(beta);
+                scal = rcp2(alpha - beta);
+            }
+#pragma unroll
+            for (int q = 0; q < E; ++q) {
+                const int i = lane + 64 * q;
+                const double v = (i <= j || i >= n) ? 0.0 : (i == j + 1 ? 1.0 : x[q] * scal);
+                if (i < NP) vs[i] = v;
+                if (i < n) V[size_t(j) * n + i] = v;
+            }
+            if (lane == 0) {
+                sh_tau = tv;
+                e[j] = beta;
+                tau[j] = tv;
+            }
+        }
+        SYTRD_STAMP(2);
+        lds_barrier();
+        SYTRD_STAMP(3);
+        const double tj = sh_tau;
+        if (tj == 0.0) {   // H_j = I (uniform): the next column is already final
+            publish_column(j + 1);
+            continue;
+        }
+        // (c) p = tau A v on the trailing block: row partials (NB independent chains), reduced over the 32
+        //     column threads of a row level by level across the rows (ILP in the DPP chain)
+        {
+            double part[NB], vcol[NB];
+#pragma unroll
+            for (int ib = 0; ib < NB; ++ib) vcol[ib] = vs[tc + GRID * ib];
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) {
+                part[ia] = 0.0;
+#pragma unroll
+                for (int ib = 0; ib < NB; ++ib) part[ia] = fma(a[ia][ib], vcol[ib], part[ia]);
+            }
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x128>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x124>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x122>(part[ia]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x121>(part[ia]);
+            if constexpr (GRID == 32) {
+#pragma unroll
+                for (int ia = 0; ia < NB; ++ia) part[ia] += xor16(part[ia]);
+            }
+            if (tc == 0) {
+#pragma unroll
+                for (int ia = 0; ia < NB; ++ia) {
+                    const int i = tr + GRID * ia;
+                    ps[i] = (i > j && i < n) ? tj * part[ia] : 0.0;
+                }
+            }
+        }
+        for (int q = NP + t; q < SY_MAX; q += GRID * GRID) ps[q] = 0.0;
+        SYTRD_STAMP(4);
+        lds_barrier();
+        SYTRD_STAMP(5);
+        // (d) every wave forms K = -(tau / 2) (p . v) itself (no extra barrier), w = p + K v on the fly;
+        //     the update's operands are read before the reduction so their LDS latency overlaps it
+        double vr[NB], pr[NB], vc[NB], pc[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            vr[q] = vs[tr + GRID * q];
+            pr[q] = ps[tr + GRID * q];
+            vc[q] = vs[tc + GRID * q];
+            pc[q] = ps[tc + GRID * q];
+        }
+        double sk = 0.0;
+#pragma unroll
+        for (int i = lane; i < NP; i += 64) sk = fma(ps[i], vs[i], sk);
+        const double K = -0.5 * tj * sum64(sk);
+        // (e) A -= v w^T + w v^T (v, w vanish at indices <= j: finished rows and columns stay untouched)
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+            const double wc = fma(K, vc[ib], pc[ib]);
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) a[ia][ib] = fma(-vr[ia], wc, fma(-fma(K, vr[ia], pr[ia]), vc[ib], a[ia][ib]));
+        }
+        publish_column(j + 1);
+    }
+#undef SYTRD_STAMP
+    // the last 2 x 2 block: d[n-2], d[n-1], e[n-2] (tau = 0, H = I)
+#pragma unroll
+    for (int ia = 0; ia < NB; ++ia)
+#pragma unroll
+        for (int ib = 0; ib < NB; ++ib) {
+            const int i = tr + GRID * ia, k = tc + GRID * ib;
+            if (n >= 2 && i == n - 2 && k == n - 2) d[n - 2] = a[ia][ib];
+            if (n >= 1 && i == n - 1 && k == n - 1) d[n - 1] = a[ia][ib];
+            if (n >= 2 && i == n - 1 && k == n - 2) {
+                e[n - 2] = a[ia][ib];
+                tau[n - 2] = 0.0;
+                for (int q = 0; q < n; ++q) V[size_t(n - 2) * n + q] = 0.0;
+            }
+        }
+}
+
+// Orders up to 256: the same column steps on a 32 x 32 grid of 1024 threads holding only the lower block
+// triangle (block (ia, ib), ib <= ia, of 32 x 32 blocks: NB (NB + 1) / 2 = 36 doubles per thread at NB = 8;
+// the full matrix would need 64, beyond the 128 VGPRs of a 1024-thread workgroup). The symmetric product
+// takes the rows of the stored blocks (reduced over the 32 column threads of a row by DPP / permlane)
+// plus, for the mirrored upper blocks, the columns of the strictly lower ones (reduced over the row threads:
+// the two of a wave by one shuffle, the 16 waves through LDS) -- one barrier more per column than the
+// full-storage kernel. The update's operands are read per row to stay within the register budget.
+template <int NB>
+__global__ void __launch_bounds__(1024) k_sytrd_lower(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
+                                                     double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V) {
+    constexpr int GRID = 32, NP = GRID * NB, NL = NB * (NB + 1) / 2, NW = GRID * GRID / 64;
+    __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX], psr[SY_MAX], cbuf[NW][SY_MAX];
+    __shared__ double sh_tau;
+    const int t = threadIdx.x, tr = t / GRID, tc = t % GRID, lane = t & 63, wave = t >> 6;
+    double a[NL];
+#pragma unroll
+    for (int ia = 0; ia < NB; ++ia)
+#pragma unroll
+        for (int ib = 0; ib <= ia; ++ib) {
+            const int i = tr + GRID * ia, k = tc + GRID * ib;
+            a[ia * (ia + 1) / 2 + ib] = (i < n && k < n) ? (i >= k ? A[size_t(i) * lda + k] : A[size_t(k) * lda + i]) : 0.0;
+        }
+    auto publish_column = [&](int j) {
+        if (tc == (j % GRID)) {
+#pragma unroll
+            for (int ia = 0; ia < NB; ++ia) {
+                const int i = tr + GRID * ia;
+#pragma unroll
+                for (int ib = 0; ib <= ia; ++ib)
+                    if (ib == (j / GRID)) {
+                        if (i > j && i < n) xs[i] = a[ia * (ia + 1) / 2 + ib];
+                        if (i == j) d[j] = a[ia * (ia + 1) / 2 + ib];
+                    }
+            }
+        }
+    };
+    publish_column(0);
+    for (int j = 0; j + 2 < n; ++j) {
+        lds_barrier();
+        if (wave == 0) {   // reflector (dlarfg), as in k_sytrd
+            constexpr int E = NP / 64;
             double x[E];
 #pragma unroll
             for (int q = 0; q < E; ++q) x[q] = xs[lane + 64 * q];
@@ -144,82 +303,77 @@ __global__ void __launch_bounds__(1024) k_sytrd(const double* __restrict__ A, in
                 tau[j] = tv;
             }
         }
-        SYTRD_STAMP(2);
         lds_barrier();
-        SYTRD_STAMP(3);
         const double tj = sh_tau;
-        if (tj == 0.0) {   // H_j = I (uniform): the next column is already final
+        if (tj == 0.0) {
             publish_column(j + 1);
             continue;
         }
-        // (c) p = tau A v on the trailing block: row partials (NB independent chains), reduced over the 32
-        //     column threads of a row level by level across the rows (ILP in the DPP chain)
+        // (c) symmetric product: row parts of the stored blocks, column parts of the strictly lower ones
         {
-            double part[NB], vcol[NB];
+            double cp[NB];
 #pragma unroll
-            for (int ib = 0; ib < NB; ++ib) vcol[ib] = vs[tc + 32 * ib];
+            for (int q = 0; q < NB; ++q) cp[q] = 0.0;
 #pragma unroll
             for (int ia = 0; ia < NB; ++ia) {
-                part[ia] = 0.0;
+                const double vrow = vs[tr + GRID * ia];
+                double rp = 0.0;
 #pragma unroll
-                for (int ib = 0; ib < NB; ++ib) part[ia] = fma(a[ia][ib], vcol[ib], part[ia]);
+                for (int ib = 0; ib <= ia; ++ib) {
+                    const double av = a[ia * (ia + 1) / 2 + ib];
+                    rp = fma(av, vs[tc + GRID * ib], rp);
+                    if (ib < ia) cp[ib] = fma(av, vrow, cp[ib]);
+                }
+                rp = sum32(rp);
+                if (tc == 0) psr[tr + GRID * ia] = rp;
             }
 #pragma unroll
-            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x128>(part[ia]);
+            for (int q = 0; q < NB; ++q) cp[q] += __shfl_xor(cp[q], 32, 64);
+            if (lane < GRID) {
 #pragma unroll
-            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x124>(part[ia]);
-#pragma unroll
-            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x122>(part[ia]);
-#pragma unroll
-            for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x121>(part[ia]);
-#pragma unroll
-            for (int ia = 0; ia < NB; ++ia) part[ia] += xor16(part[ia]);
-            if (tc == 0) {
-#pragma unroll
-                for (int ia = 0; ia < NB; ++ia) {
-                    const int i = tr + 32 * ia;
-                    ps[i] = (i > j && i < n) ? tj * part[ia] : 0.0;
-                }
+                for (int q = 0; q < NB; ++q) cbuf[wave][tc + GRID * q] = cp[q];
             }
         }
-        if (t < SY_MAX && t >= 32 * NB) ps[t] = 0.0;
-        SYTRD_STAMP(4);
         lds_barrier();
-        SYTRD_STAMP(5);
-        // (d) every wave forms K = -(tau / 2) (p . v) itself (no extra barrier), w = p + K v on the fly;
-        //     the update's operands are read before the reduction so their LDS latency overlaps it
-        double vr[NB], pr[NB], vc[NB], pc[NB];
+        if (t < SY_MAX) {
+            double c = 0.0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) c += cbuf[w][t];
+            ps[t] = (t > j && t < n) ? tj * (psr[t] + c) : 0.0;
+        }
+        lds_barrier();
+        // (d) + (e) as in k_sytrd, on the stored blocks
+        double sk = 0.0;
+        for (int i = lane; i < NP; i += 64) sk = fma(ps[i], vs[i], sk);
+        const double K = -0.5 * tj * sum64(sk);
+        double vc[NB], wc[NB];
 #pragma unroll
         for (int q = 0; q < NB; ++q) {
-            vr[q] = vs[tr + 32 * q];
-            pr[q] = ps[tr + 32 * q];
-            vc[q] = vs[tc + 32 * q];
-            pc[q] = ps[tc + 32 * q];
+            vc[q] = vs[tc + GRID * q];
+            wc[q] = fma(K, vc[q], ps[tc + GRID * q]);
         }
-        double sk = 0.0;
 #pragma unroll
-        for (int q = 0; q < NB / 2; ++q) sk = fma(ps[lane + 64 * q], vs[lane + 64 * q], sk);
-        const double K = -0.5 * tj * sum64(sk);
-        // (e) A -= v w^T + w v^T (v, w vanish at indices <= j: finished rows and columns stay untouched)
+        for (int ia = 0; ia < NB; ++ia) {
+            const double vr = vs[tr + GRID * ia];
+            const double wr = fma(K, vr, ps[tr + GRID * ia]);
 #pragma unroll
-        for (int ib = 0; ib < NB; ++ib) {
-            const double wc = fma(K, vc[ib], pc[ib]);
-#pragma unroll
-            for (int ia = 0; ia < NB; ++ia) a[ia][ib] = fma(-vr[ia], wc, fma(-fma(K, vr[ia], pr[ia]), vc[ib], a[ia][ib]));
+            for (int ib = 0; ib <= ia; ++ib) {
+                double& av = a[ia * (ia + 1) / 2 + ib];
+                av = fma(-vr, wc[ib], fma(-wr, vc[ib], av));
+            }
         }
         publish_column(j + 1);
     }
-#undef SYTRD_STAMP
-    // the last 2 x 2 block: d[n-2], d[n-1], e[n-2] (tau = 0, H = I)
 #pragma unroll
     for (int ia = 0; ia < NB; ++ia)
 #pragma unroll
-        for (int ib = 0; ib < NB; ++ib) {
-            const int i = tr + 32 * ia, k = tc + 32 * ib;
-            if (n >= 2 && i == n - 2 && k == n - 2) d[n - 2] = a[ia][ib];
-            if (n >= 1 && i == n - 1 && k == n - 1) d[n - 1] = a[ia][ib];
+        for (int ib = 0; ib <= ia; ++ib) {
+            const int i = tr + GRID * ia, k = tc + GRID * ib;
+            const double av = a[ia * (ia + 1) / 2 + ib];
+            if (n >= 2 && i == n - 2 && k == n - 2) d[n - 2] = av;
+            if (n >= 1 && i == n - 1 && k == n - 1) d[n - 1] = av;
             if (n >= 2 && i == n - 1 && k == n - 2) {
-                e[n - 2] = a[ia][ib];
+                e[n - 2] = av;
                 tau[n - 2] = 0.0;
                 for (int q = 0; q < n; ++q) V[size_t(n - 2) * n + q] = 0.0;
             }
@@ -373,42 +527,49 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
 }
 
 // u = H_0 H_1 ... H_{n-2} z for every row z of Zt (in place): 16 vectors per 256-thread workgroup, 16 lanes
-// per vector holding n / 16 entries each
+// per vector holding n / 16 entries each; the reflectors pass through LDS in chunks of 16384 / n rows
+// (all of them at once up to n = 128), staged by the whole workgroup with coalesced loads
+template <int ZE>
 __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, const double* __restrict__ tau, int n, int kk,
                                                double* __restrict__ Zt, int ldz) {
-    // every reflector and tau staged in LDS once (n <= 128: 128 KB), read per application by 16 lanes each
-    __shared__ double sv[128 * 128 + 128];
-    for (int e = threadIdx.x; e < (n - 1) * n; e += 256) sv[e] = V[e];
-    for (int e = threadIdx.x; e < n; e += 256) sv[128 * 128 + e] = e + 1 < n ? tau[e] : 0.0;
-    __syncthreads();
+    constexpr int CHUNK_ELEMS = 16384;
+    __shared__ double sv[CHUNK_ELEMS], st[SY_MAX];
+    for (int e = threadIdx.x; e < n; e += 256) st[e] = e + 1 < n ? tau[e] : 0.0;
     const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
     const int q = blockIdx.x * 16 + g;
     const bool live = q < kk;
-    double z[128 / 16];
+    double z[ZE];
 #pragma unroll
-    for (int s = 0; s < 128 / 16; ++s) {
+    for (int s = 0; s < ZE; ++s) {
         const int i = l + 16 * s;
         z[s] = (live && i < n) ? Zt[size_t(q) * ldz + i] : 0.0;
     }
-    for (int j = n - 2; j >= 0; --j) {
-        const double tj = sv[128 * 128 + j];
-        if (tj == 0.0) continue;
-        const double* v = sv + size_t(j) * n;
-        double vv[128 / 16];
-        double dot = 0.0;
+    const int rows = CHUNK_ELEMS / n;
+    for (int hi = n - 2; hi >= 0; hi -= rows) {
+        const int lo = hi - rows + 1 > 0 ? hi - rows + 1 : 0;
+        __syncthreads();
+        for (int e = threadIdx.x; e < (hi - lo + 1) * n; e += 256) sv[e] = V[size_t(lo) * n + e];
+        __syncthreads();
+        for (int j = hi; j >= lo; --j) {
+            const double tj = st[j];
+            if (tj == 0.0) continue;
+            const double* v = sv + size_t(j - lo) * n;
+            double vv[ZE];
+            double dot = 0.0;
 #pragma unroll
-        for (int s = 0; s < 128 / 16; ++s) {
-            const int i = l + 16 * s;
-            vv[s] = i < n ? v[i] : 0.0;
-            dot = fma(vv[s], z[s], dot);
+            for (int s = 0; s < ZE; ++s) {
+                const int i = l + 16 * s;
+                vv[s] = i < n ? v[i] : 0.0;
+                dot = fma(vv[s], z[s], dot);
+            }
+            const double f = tj * sum16(dot);
+#pragma unroll
+            for (int s = 0; s < ZE; ++s) z[s] = fma(-f, vv[s], z[s]);
         }
-        const double f = tj * sum16(dot);
-#pragma unroll
-        for (int s = 0; s < 128 / 16; ++s) z[s] = fma(-f, vv[s], z[s]);
     }
     if (live) {
 #pragma unroll
-        for (int s = 0; s < 128 / 16; ++s) {
+        for (int s = 0; s < ZE; ++s) {
             const int i = l + 16 * s;
             if (i < n) Zt[size_t(q) * ldz + i] = z[s];
         }
@@ -422,12 +583,16 @@ __global__ void k_sqrt_lam(const double* __restrict__ lam, int kk, double* __res
 
 }  // namespace
 
-// (n <= 128: the register grid holds 16 doubles per thread; 256 would need 64, beyond the 128 VGPRs of a
-// 1024-thread workgroup)
-bool sym_eig_top_fits(int n, int kk) { return n >= 2 && n <= 128 && kk >= 1 && kk <= n; }
+// Default order limit 128: the lower-block kernel for 129..256 spills 324 B per lane (36 doubles of matrix +
+// the symmetric product's column partials exceed 128 VGPRs) and measured 5.8 ms per 256-order edge against
+// 2.7 ms of Jacobi sweeps (profiles/r03/sum128_eig_kernel_stats_r03q.csv); XRS_SYEV_MAX=256 enables it.
+bool sym_eig_top_fits(int n, int kk) {
+    static const int nmax = std::getenv("XRS_SYEV_MAX") ? std::atoi(std::getenv("XRS_SYEV_MAX")) : 128;
+    return n >= 2 && n <= std::min(nmax, SY_MAX) && kk >= 1 && kk <= n;
+}
 
 void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status) {
-    XRS_REQUIRE(sym_eig_top_fits(n, kk), "sym_eig_top: need 2 <= n <= 256 and 1 <= kk <= n");
+XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <= n <= 256 and 1 <= kk <= n");
     DevBuf dbuf(h, size_t(n) * 8), ebuf(h, size_t(n) * 8), tbuf(h, size_t(n) * 8), V(h, size_t(n) * n * 8), lbuf(h, size_t(kk) * 8);
     double* lm = lam ? lam : lbuf.d();
     KernelTimer timer(h, XRS_KFAM_SVD, 4.0 / 3.0 * double(n) * n * n + 4.0 * double(n) * n * kk, 8.0 * double(n) * n * 2);
@@ -435,12 +600,21 @@ void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double
     DevBuf sb(h, want_stamps ? 768 * 8 : 0);
     unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
     if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 768 * 8, h->stream));
-    if (n <= 64) hipLaunchKernelGGL((k_sytrd<2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
-    else hipLaunchKernelGGL((k_sytrd<4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
+    // the 1024-thread grid up to 128 (measured faster than 256 threads with 64 elements each: 5.1 vs 5.6 ms
+    // per cfg3 round(64), profiles/r03/sytrd_grid_ab_r03q.txt -- one wave per SIMD is issue-bound in the
+    // update), the lower-block 1024-thread grid above
+    if (n <= 64) {
+        hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
+    } else if (n <= 128) {
+        hipLaunchKernelGGL((k_sytrd<32, 4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
+    } else {
+        hipLaunchKernelGGL((k_sytrd_lower<8>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
+    }
     check_launch("k_sytrd");
     hipLaunchKernelGGL(k_stebz_stein, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
     check_launch("k_stebz_stein");
-    hipLaunchKernelGGL(k_ormtr, dim3((kk + 15) / 16), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    if (n <= 128) hipLaunchKernelGGL((k_ormtr<8>), dim3((kk + 15) / 16), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    else hipLaunchKernelGGL((k_ormtr<16>), dim3((kk + 15) / 16), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     check_launch("k_ormtr");
     if (stp) {   // per-phase cycles of the first steps: (b)-wait, reflector, wait, symv, wait, update (+ column)
         std::vector<unsigned long long> hst(768);
