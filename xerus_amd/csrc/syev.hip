@@ -10,6 +10,10 @@
 //   2. k_stebz_stein: one wave per wanted eigenvalue (kk workgroups in parallel): Sturm-count
 //      multisection on 64 points per round (~9 rounds to full precision), then inverse iteration with the
 //      partially pivoted LU of T - lambda I (dgttrf / dgttrs), three solves from a fixed start vector.
+//      Measured alternatives (profiles/r03/stein_variants_r03r.txt): a single twisted-factorisation solve
+//      (orthogonality only 1e-12..1e-11 on flat spectra, T - lambda I not being a relatively robust
+//      representation); 4 waves with 512 points per round and register-prefetched chains (6 instead of 9
+//      rounds, same 105 us: every O(n) chain is bound by its ~20-cycle dependent FP64 latency per level).
 //   3. k_ormtr: the eigenvectors back to A's coordinates, u = H_0 ... H_{n-2} z, 16 vectors per workgroup
 //      (16 lanes each), the reflectors read from L2.
 // Inverse iteration is accurate for eigenvalues separated relative to ||T|| (the certified rounds' random

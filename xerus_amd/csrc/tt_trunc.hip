@@ -320,12 +320,21 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     nst = 0;
     XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
     std::vector<int*> jst;   // Jacobi statuses
+    // certificates of the eigensolver edges on side stream 0 (off the sweep's critical path), when this
+    // handle owns its streams and is not inside a fork
+    static const bool cert_side_env = std::getenv("XRS_TRUNC_CERT_INLINE") == nullptr;
+    const bool cert_side = cert_side_env && !h->borrowed_streams && h->stream == h->own_stream && h->side_stream[0];
+    bool side_used = false;
     for (size_t k = d - 1; k >= 1; --k) {
         const size_t r = rr[k], N = t.n[k] * rr[k + 1], Ng = ng[k] * rr[k + 1];   // local / global columns
         const size_t kk = std::min({r, Ng, max_ranks[k - 1]});
         const bool wide = r <= Ng;
         if (!wide && t.sharded()) {   // the N x N Gram of a tall edge spans the ranks' column blocks
             if (dbg) std::fprintf(stderr, "round_truncate: sharded tall edge %zu -> not certified\n", k);
+            if (side_used) {   // the side stream may still read this sweep's buffers
+                XRS_HIP(hipEventRecord(h->ev_join[0], h->side_stream[0]));
+                XRS_HIP(hipStreamWaitEvent(h->stream, h->ev_join[0], 0));
+            }
             sw.discard();
             return false;
         }
@@ -344,10 +353,31 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         const bool use_eig = !force_jacobi && sym_eig_top_fits(int(g), int(kk));
         double* L = use_eig ? nullptr : sw.buf(g * g);
         double* Z = (!use_eig && g > 256) ? sw.buf(g * g) : nullptr;   // (factor_big always builds L^{-1})
-        std::vector<CholJob> cj{{P, int(g), nullptr, nullptr}};
-        if (!use_eig) cj.insert(cj.begin(), CholJob{P, int(g), L, Z});
-        chol_jobs(sw, cj, status + nst);
-        nst += chol_status_count(cj);
+        if (use_eig && cert_side) {
+            // the eigensolver does not need the factor: the status-only certificate runs on a side stream
+            // beside it (its status is read after the one join before the final check)
+            double* dinv = sw.buf(dinv_elems(int(g)));
+            PotrfBatch pb{};
+            pb.src[0] = P;
+            pb.G[0] = nullptr;
+            pb.Dinv[0] = dinv;
+            pb.shift[0] = -kGramShift;
+            pb.n[0] = int(g);
+            pb.status = status + nst;
+            XRS_HIP(hipEventRecord(h->ev_fork, h->stream));
+            XRS_HIP(hipStreamWaitEvent(h->side_stream[0], h->ev_fork, 0));
+            hipStream_t main_stream = h->stream;
+            h->stream = h->side_stream[0];
+            potrf_batched(h, pb, 1);
+            h->stream = main_stream;
+            side_used = true;
+            nst += 1;
+        } else {
+            std::vector<CholJob> cj{{P, int(g), nullptr, nullptr}};
+            if (!use_eig) cj.insert(cj.begin(), CholJob{P, int(g), L, Z});
+            chol_jobs(sw, cj, status + nst);
+            nst += chol_status_count(cj);
+        }
         double* S = sw.buf(g);
         double* Vt = wide ? sw.buf(g * g) : sw.core(g * g);
         int* js = status + kJacobiSlot + int(jst.size());
@@ -375,6 +405,10 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         A[k] = newk;
         A[k - 1] = prevk;
         rr[k] = kk;
+    }
+    if (side_used) {   // join: the side stream's certificates before the statuses are read
+        XRS_HIP(hipEventRecord(h->ev_join[0], h->side_stream[0]));
+        XRS_HIP(hipStreamWaitEvent(h->stream, h->ev_join[0], 0));
     }
     // right-orthonormality of the new cores 1..d-1
     {
