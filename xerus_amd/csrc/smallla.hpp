@@ -69,7 +69,7 @@ bool jacobi_vt_fits_lds(int p, int q);
 // eigenvalue, back-transformation (syev.hip). lam (kk, optional) descending, S = sqrt(max(lam, 0))
 // (optional), Ut rows = the eigenvectors (kk x n, row stride ldu). *status_dev set to -1 if a
 // multisection did not converge (left untouched otherwise). Enqueued only.
-bool sym_eig_top_fits(int n, int kk);   // the truncating round's policy (n <= 128 unless XRS_SYEV_MAX)
+bool sym_eig_top_fits(int n, int kk);   // the truncating round's policy (n <= 256 unless XRS_SYEV_MAX lowers it)
 void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status_dev);
 bool jacobi_usv_fits(int p, int q);
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,

@@ -155,11 +155,7 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
         SYTRD_STAMP(2);
         lds_barrier();
         SYTRD_STAMP(3);
-        const double tj = sh_tau;
-        if (tj == 0.0) {   // H_j = I (uniform): the next column is already final
-            publish_column(j + 1);
-            continue;
-        }
+        const double tj = sh_tau;   // (tau = 0: p = w = 0, the update leaves A unchanged; no second latch)
         // (c) p = tau A v on the trailing block: row partials (NB independent chains), reduced over the 32
         //     column threads of a row level by level across the rows (ILP in the DPP chain)
         {
@@ -236,43 +232,60 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
         }
 }
 
-// Orders up to 256: the same column steps on a 32 x 32 grid of 1024 threads holding only the lower block
-// triangle (block (ia, ib), ib <= ia, of 32 x 32 blocks: NB (NB + 1) / 2 = 36 doubles per thread at NB = 8;
-// the full matrix would need 64, beyond the 128 VGPRs of a 1024-thread workgroup). The symmetric product
-// takes the rows of the stored blocks (reduced over the 32 column threads of a row by DPP / permlane)
-// plus, for the mirrored upper blocks, the columns of the strictly lower ones (reduced over the row threads:
-// the two of a wave by one shuffle, the 16 waves through LDS) -- one barrier more per column than the
-// full-storage kernel. The update's operands are read per row to stay within the register budget.
-template <int NB>
-__global__ void __launch_bounds__(1024) k_sytrd_lower(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
-                                                     double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V) {
-    constexpr int GRID = 32, NP = GRID * NB, NL = NB * (NB + 1) / 2, NW = GRID * GRID / 64;
+// Orders 129..256: the same column steps on 512 threads (8 waves, two per SIMD: 256 VGPRs each) holding
+// the lower triangle by blocks. Thread (tr, tc) = (t / 16, t % 16) of a 32 x 16 grid owns the elements
+// (tr + 32 ia, tc + 16 ib) of the blocks with ib <= 2 ia + 1 (the ones meeting the lower triangle:
+// 72 doubles); the entries above the diagonal in the two diagonal-crossing blocks of a block row stay zero.
+// The symmetric product sums the rows of the stored entries (over the 16 column threads of a row: one DPP
+// row) plus, for the mirrored upper triangle, the columns of the strictly lower ones (over the 4 rows of a
+// wave by permlane16 / shuffle, then over the 8 waves through LDS). The column halves (ib < 8, ib >= 8) are
+// processed one after the other to bound the live operand registers.
+__global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
+                                                   double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V) {
+    constexpr int NR = 8, NW = 8, NP = 256;
+    constexpr int NL = NR * (NR + 1);   // block row ia holds column blocks 0 .. 2 ia + 1: offset ia (ia + 1)
     __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX], psr[SY_MAX], cbuf[NW][SY_MAX];
     __shared__ double sh_tau;
-    const int t = threadIdx.x, tr = t / GRID, tc = t % GRID, lane = t & 63, wave = t >> 6;
+    const int t = threadIdx.x, tr = t >> 4, tc = t & 15, lane = t & 63, wave = t >> 6;
+    // diagonal-crossing blocks of block row ia: ib = 2 ia (i - k = tr - tc), ib = 2 ia + 1 (i - k = tr - tc - 16)
+    const bool keep0 = tr >= tc, keep1 = tr >= tc + 16;   // on or below the diagonal
+    const bool low0 = tr > tc, low1 = tr > tc + 16;       // strictly below
     double a[NL];
 #pragma unroll
-    for (int ia = 0; ia < NB; ++ia)
+    for (int ia = 0; ia < NR; ++ia)
 #pragma unroll
-        for (int ib = 0; ib <= ia; ++ib) {
-            const int i = tr + GRID * ia, k = tc + GRID * ib;
-            a[ia * (ia + 1) / 2 + ib] = (i < n && k < n) ? (i >= k ? A[size_t(i) * lda + k] : A[size_t(k) * lda + i]) : 0.0;
+        for (int ib = 0; ib <= 2 * ia + 1; ++ib) {
+            const int i = tr + 32 * ia, k = tc + 16 * ib;
+            const bool keep = (ib < 2 * ia || (ib == 2 * ia ? keep0 : keep1)) && i < n && k < n;
+            const double x = A[size_t(keep ? i : 0) * lda + (keep ? k : 0)];
+            a[ia * (ia + 1) + ib] = keep ? x : 0.0;
         }
-    auto publish_column = [&](int j) {
-        if (tc == (j % GRID)) {
-#pragma unroll
-            for (int ia = 0; ia < NB; ++ia) {
-                const int i = tr + GRID * ia;
-#pragma unroll
-                for (int ib = 0; ib <= ia; ++ib)
-                    if (ib == (j / GRID)) {
-                        if (i > j && i < n) xs[i] = a[ia * (ia + 1) / 2 + ib];
-                        if (i == j) d[j] = a[ia * (ia + 1) / 2 + ib];
-                    }
-            }
-        }
-    };
-    publish_column(0);
+    // column jj of the current matrix to LDS (xs) and its diagonal entry to d, by the column's owners
+#define L512_PUBLISH_CASE(IB)                                                             \
+    case IB:                                                                              \
+        _Pragma("unroll") for (int ia = (IB) / 2; ia < NR; ++ia) {                        \
+            const int i = tr + 32 * ia;                                                   \
+            const double av = a[ia * (ia + 1) + (IB)];                                    \
+            if (i > pj && i < n) xs[i] = av;                                              \
+            if (i == pj) d[pj] = av;                                                      \
+        }                                                                                 \
+        break;
+#define L512_PUBLISH(jj)                                                                  \
+    do {                                                                                  \
+        const int pj = (jj);                                                              \
+        if (tc == (pj & 15)) {                                                            \
+            switch (pj >> 4) {                                                            \
+                L512_PUBLISH_CASE(0) L512_PUBLISH_CASE(1) L512_PUBLISH_CASE(2)            \
+                L512_PUBLISH_CASE(3) L512_PUBLISH_CASE(4) L512_PUBLISH_CASE(5)            \
+                L512_PUBLISH_CASE(6) L512_PUBLISH_CASE(7) L512_PUBLISH_CASE(8)            \
+                L512_PUBLISH_CASE(9) L512_PUBLISH_CASE(10) L512_PUBLISH_CASE(11)          \
+                L512_PUBLISH_CASE(12) L512_PUBLISH_CASE(13) L512_PUBLISH_CASE(14)         \
+                L512_PUBLISH_CASE(15)                                                     \
+                default: break;                                                           \
+            }                                                                             \
+        }                                                                                 \
+    } while (0)
+    L512_PUBLISH(0);
     for (int j = 0; j + 2 < n; ++j) {
         lds_barrier();
         if (wave == 0) {   // reflector (dlarfg), as in k_sytrd
@@ -308,35 +321,50 @@ __global__ void __launch_bounds__(1024) k_sytrd_lower(const double* __restrict__
             }
         }
         lds_barrier();
+        // (no early exit for tau = 0: p = w = 0 then and the update leaves every entry unchanged; a second
+        // loop latch would double the live matrix registers at the merge)
         const double tj = sh_tau;
-        if (tj == 0.0) {
-            publish_column(j + 1);
-            continue;
-        }
-        // (c) symmetric product: row parts of the stored blocks, column parts of the strictly lower ones
-        {
-            double cp[NB];
+        // symmetric product: row sums of the stored entries, column sums of the strictly lower ones
+        double rp[NR];
 #pragma unroll
-            for (int q = 0; q < NB; ++q) cp[q] = 0.0;
+        for (int ia = 0; ia < NR; ++ia) rp[ia] = 0.0;
 #pragma unroll
-            for (int ia = 0; ia < NB; ++ia) {
-                const double vrow = vs[tr + GRID * ia];
-                double rp = 0.0;
+        for (int hh = 0; hh < 2; ++hh) {
+            double cp[8], vk[8];
 #pragma unroll
-                for (int ib = 0; ib <= ia; ++ib) {
-                    const double av = a[ia * (ia + 1) / 2 + ib];
-                    rp = fma(av, vs[tc + GRID * ib], rp);
-                    if (ib < ia) cp[ib] = fma(av, vrow, cp[ib]);
+            for (int q = 0; q < 8; ++q) {
+                cp[q] = 0.0;
+                vk[q] = vs[tc + 16 * (8 * hh + q)];
+            }
+#pragma unroll
+            for (int ia = 0; ia < NR; ++ia) {
+                __builtin_amdgcn_sched_barrier(0);
+                const double vi = vs[tr + 32 * ia];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int ib = 8 * hh + q;
+                    if (ib <= 2 * ia + 1) {
+                        const double av = a[ia * (ia + 1) + ib];
+                        rp[ia] = fma(av, vk[q], rp[ia]);
+                        if (ib < 2 * ia) cp[q] = fma(av, vi, cp[q]);
+                        else cp[q] = fma((ib == 2 * ia ? low0 : low1) ? av : 0.0, vi, cp[q]);
+                    }
                 }
-                rp = sum32(rp);
-                if (tc == 0) psr[tr + GRID * ia] = rp;
             }
 #pragma unroll
-            for (int q = 0; q < NB; ++q) cp[q] += __shfl_xor(cp[q], 32, 64);
-            if (lane < GRID) {
-#pragma unroll
-                for (int q = 0; q < NB; ++q) cbuf[wave][tc + GRID * q] = cp[q];
+            for (int q = 0; q < 8; ++q) {
+                cp[q] += xor16(cp[q]);
+                cp[q] += __shfl_xor(cp[q], 32, 64);
             }
+            if (lane < 16) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) cbuf[wave][tc + 16 * (8 * hh + q)] = cp[q];
+            }
+        }
+#pragma unroll
+        for (int ia = 0; ia < NR; ++ia) {
+            const double r = sum16(rp[ia]);
+            if (tc == 0) psr[tr + 32 * ia] = r;
         }
         lds_barrier();
         if (t < SY_MAX) {
@@ -346,37 +374,45 @@ __global__ void __launch_bounds__(1024) k_sytrd_lower(const double* __restrict__
             ps[t] = (t > j && t < n) ? tj * (psr[t] + c) : 0.0;
         }
         lds_barrier();
-        // (d) + (e) as in k_sytrd, on the stored blocks
+        // K = -(tau / 2) (p . v) in every wave, w = p + K v on the fly; A -= v w^T + w v^T on the kept entries
         double sk = 0.0;
-        for (int i = lane; i < NP; i += 64) sk = fma(ps[i], vs[i], sk);
+#pragma unroll
+        for (int q = 0; q < NP / 64; ++q) sk = fma(ps[lane + 64 * q], vs[lane + 64 * q], sk);
         const double K = -0.5 * tj * sum64(sk);
-        double vc[NB], wc[NB];
+        {
+            double vi[NR], wi[NR];
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            vc[q] = vs[tc + GRID * q];
-            wc[q] = fma(K, vc[q], ps[tc + GRID * q]);
-        }
+            for (int ia = 0; ia < NR; ++ia) {
+                vi[ia] = vs[tr + 32 * ia];
+                wi[ia] = fma(K, vi[ia], ps[tr + 32 * ia]);
+            }
 #pragma unroll
-        for (int ia = 0; ia < NB; ++ia) {
-            const double vr = vs[tr + GRID * ia];
-            const double wr = fma(K, vr, ps[tr + GRID * ia]);
+            for (int ib = 0; ib < 16; ++ib) {
+                __builtin_amdgcn_sched_barrier(0);   // one column block at a time (hoisted operands spill)
+                const double vk = vs[tc + 16 * ib];
+                const double wk = fma(K, vk, ps[tc + 16 * ib]);
 #pragma unroll
-            for (int ib = 0; ib <= ia; ++ib) {
-                double& av = a[ia * (ia + 1) / 2 + ib];
-                av = fma(-vr, wc[ib], fma(-wr, vc[ib], av));
+                for (int ia = ib / 2; ia < NR; ++ia) {
+                    const int ix = ia * (ia + 1) + ib;
+                    const double u = fma(-vi[ia], wk, fma(-wi[ia], vk, a[ix]));
+                    a[ix] = (ib < 2 * ia || (ib == 2 * ia ? keep0 : keep1)) ? u : 0.0;
+                }
             }
         }
-        publish_column(j + 1);
+        L512_PUBLISH(j + 1);
     }
+#undef L512_PUBLISH
+#undef L512_PUBLISH_CASE
+    // the last 2 x 2 block: d[n-2], d[n-1], e[n-2] (tau = 0, H = I)
 #pragma unroll
-    for (int ia = 0; ia < NB; ++ia)
+    for (int ia = 0; ia < NR; ++ia)
 #pragma unroll
-        for (int ib = 0; ib <= ia; ++ib) {
-            const int i = tr + GRID * ia, k = tc + GRID * ib;
-            const double av = a[ia * (ia + 1) / 2 + ib];
-            if (n >= 2 && i == n - 2 && k == n - 2) d[n - 2] = av;
-            if (n >= 1 && i == n - 1 && k == n - 1) d[n - 1] = av;
-            if (n >= 2 && i == n - 1 && k == n - 2) {
+        for (int ib = 0; ib <= 2 * ia + 1; ++ib) {
+            const int i = tr + 32 * ia, k = tc + 16 * ib;
+            const double av = a[ia * (ia + 1) + ib];
+            if (i == n - 2 && k == n - 2) d[n - 2] = av;
+            if (i == n - 1 && k == n - 1) d[n - 1] = av;
+            if (i == n - 1 && k == n - 2) {
                 e[n - 2] = av;
                 tau[n - 2] = 0.0;
                 for (int q = 0; q < n; ++q) V[size_t(n - 2) * n + q] = 0.0;
@@ -587,11 +623,12 @@ __global__ void k_sqrt_lam(const double* __restrict__ lam, int kk, double* __res
 
 }  // namespace
 
-// Default order limit 128: the lower-block kernel for 129..256 spills 324 B per lane (36 doubles of matrix +
-// the symmetric product's column partials exceed 128 VGPRs) and measured 5.8 ms per 256-order edge against
-// 2.7 ms of Jacobi sweeps (profiles/r03/sum128_eig_kernel_stats_r03q.csv); XRS_SYEV_MAX=256 enables it.
+// Order limit 256 (XRS_SYEV_MAX lowers it): the 512-thread lower-block kernel runs an order-256 edge in
+// 1.31 ms against 2.8 ms of Jacobi sweeps ((x + y).round(128): 22.5 -> 13.8 ms, profiles/r03/sum128_l512_r03s.txt).
+// Its first version spilled (the tau = 0 early exit gave the column loop a second latch, and the register
+// copies at the merge doubled the live matrix): 3.6 ms; the spilling 1024-thread variant measured 5.8 ms.
 bool sym_eig_top_fits(int n, int kk) {
-    static const int nmax = std::getenv("XRS_SYEV_MAX") ? std::atoi(std::getenv("XRS_SYEV_MAX")) : 128;
+    static const int nmax = std::getenv("XRS_SYEV_MAX") ? std::atoi(std::getenv("XRS_SYEV_MAX")) : 256;
     return n >= 2 && n <= std::min(nmax, SY_MAX) && kk >= 1 && kk <= n;
 }
 
@@ -606,13 +643,13 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 768 * 8, h->stream));
     // the 1024-thread grid up to 128 (measured faster than 256 threads with 64 elements each: 5.1 vs 5.6 ms
     // per cfg3 round(64), profiles/r03/sytrd_grid_ab_r03q.txt -- one wave per SIMD is issue-bound in the
-    // update), the lower-block 1024-thread grid above
+    // update), the 512-thread lower-block grid above
     if (n <= 64) {
         hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
     } else if (n <= 128) {
         hipLaunchKernelGGL((k_sytrd<32, 4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
     } else {
-        hipLaunchKernelGGL((k_sytrd_lower<8>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
+        hipLaunchKernelGGL(k_sytrd_l512, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
     }
     check_launch("k_sytrd");
     hipLaunchKernelGGL(k_stebz_stein, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
