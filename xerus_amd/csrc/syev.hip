@@ -14,8 +14,8 @@
 //      (orthogonality only 1e-12..1e-11 on flat spectra, T - lambda I not being a relatively robust
 //      representation); 4 waves with 512 points per round and register-prefetched chains (6 instead of 9
 //      rounds, same 105 us: every O(n) chain is bound by its ~20-cycle dependent FP64 latency per level).
-//   3. k_ormtr: the eigenvectors back to A's coordinates, u = H_0 ... H_{n-2} z, 16 vectors per workgroup
-//      (16 lanes each), the reflectors read from L2.
+//   3. k_ormtr: the eigenvectors back to A's coordinates, u = H_0 ... H_{n-2} z, one wave per vector
+//      (64 lanes, 4 vectors per workgroup), the reflectors staged through LDS in chunks.
 // Inverse iteration is accurate for eigenvalues separated relative to ||T|| (the certified rounds' random
 // spectra); a cluster would give non-orthogonal vectors, which the round's final orthonormality check
 // rejects (then the reference's algorithm runs).
@@ -35,7 +35,7 @@ constexpr int SY_MAX = 256;
 
 // Cross-lane sums without the LDS crossbar (a __shfl_xor of a double is two ds_bpermute round trips, the
 // bulk of a column step when chained): DPP row rotations within 16 lanes, v_permlane16_swap across the
-// two rows of a 32-lane half, one shuffle across the halves.
+// two rows of a 32-lane half, v_permlane32_swap across the halves.
 template <int CTRL>
 __device__ __forceinline__ double dpp(double v) {
     const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
@@ -55,7 +55,12 @@ __device__ __forceinline__ double sum16(double v) {   // every lane of the 16-la
     return v;
 }
 __device__ __forceinline__ double sum32(double v) { v = sum16(v); return v + xor16(v); }
-__device__ __forceinline__ double sum64(double v) { v = sum32(v); return v + __shfl_xor(v, 32, 64); }
+__device__ __forceinline__ double xor32(double v) {   // the value of lane l ^ 32 (v_permlane32_swap)
+    const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return (threadIdx.x & 32) ? __hiloint2double(hi[0], lo[0]) : __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double sum64(double v) { v = sum32(v); return v + xor32(v); }
 
 // workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
 // stores (__syncthreads' release fence would drain the per-column stores of the reflectors, d, e and tau
@@ -354,7 +359,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 cp[q] += xor16(cp[q]);
-                cp[q] += __shfl_xor(cp[q], 32, 64);
+                cp[q] += xor32(cp[q]);
             }
             if (lane < 16) {
 #pragma unroll
@@ -566,22 +571,26 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     for (int i = lane; i < n; i += 64) Zt[size_t(q) * ldz + i] = lb[i];
 }
 
-// u = H_0 H_1 ... H_{n-2} z for every row z of Zt (in place): 16 vectors per 256-thread workgroup, 16 lanes
-// per vector holding n / 16 entries each; the reflectors pass through LDS in chunks of 16384 / n rows
-// (all of them at once up to n = 128), staged by the whole workgroup with coalesced loads
+
+// u = H_0 H_1 ... H_{n-2} z for every row z of Zt (in place): one wave per vector (entry i on lane i mod
+// 64, ZE = n / 64 per lane), 4 vectors per 256-thread workgroup, so the dependent chain per reflector is
+// two FMAs, a 64-lane reduction without the LDS crossbar (DPP, permlane16 / permlane32 swaps) and one
+// FMA; the reflectors pass through LDS in chunks of 16384 / n rows, staged by the whole workgroup with
+// coalesced loads. (The first version, 16 lanes per vector and 16 vectors per workgroup, ran a 16-deep
+// FMA chain per reflector on only kk / 16 workgroups: 150 us at n = 256, kk = 128.)
 template <int ZE>
 __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, const double* __restrict__ tau, int n, int kk,
                                                double* __restrict__ Zt, int ldz) {
     constexpr int CHUNK_ELEMS = 16384;
     __shared__ double sv[CHUNK_ELEMS], st[SY_MAX];
     for (int e = threadIdx.x; e < n; e += 256) st[e] = e + 1 < n ? tau[e] : 0.0;
-    const int g = threadIdx.x >> 4, l = threadIdx.x & 15;
-    const int q = blockIdx.x * 16 + g;
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     const bool live = q < kk;
     double z[ZE];
 #pragma unroll
     for (int s = 0; s < ZE; ++s) {
-        const int i = l + 16 * s;
+        const int i = lane + 64 * s;
         z[s] = (live && i < n) ? Zt[size_t(q) * ldz + i] : 0.0;
     }
     const int rows = CHUNK_ELEMS / n;
@@ -590,19 +599,19 @@ __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, con
         __syncthreads();
         for (int e = threadIdx.x; e < (hi - lo + 1) * n; e += 256) sv[e] = V[size_t(lo) * n + e];
         __syncthreads();
-        for (int j = hi; j >= lo; --j) {
-            const double tj = st[j];
-            if (tj == 0.0) continue;
+#pragma unroll 2
+        for (int j = hi; j >= lo; --j) {   // (tau_j = 0: f = 0, z unchanged)
             const double* v = sv + size_t(j - lo) * n;
             double vv[ZE];
-            double dot = 0.0;
+            double d0 = 0.0, d1 = 0.0;
 #pragma unroll
             for (int s = 0; s < ZE; ++s) {
-                const int i = l + 16 * s;
+                const int i = lane + 64 * s;
                 vv[s] = i < n ? v[i] : 0.0;
-                dot = fma(vv[s], z[s], dot);
+                if (s & 1) d1 = fma(vv[s], z[s], d1);
+                else d0 = fma(vv[s], z[s], d0);
             }
-            const double f = tj * sum16(dot);
+            const double f = st[j] * sum64(d0 + d1);
 #pragma unroll
             for (int s = 0; s < ZE; ++s) z[s] = fma(-f, vv[s], z[s]);
         }
@@ -610,7 +619,7 @@ __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, con
     if (live) {
 #pragma unroll
         for (int s = 0; s < ZE; ++s) {
-            const int i = l + 16 * s;
+            const int i = lane + 64 * s;
             if (i < n) Zt[size_t(q) * ldz + i] = z[s];
         }
     }
@@ -654,8 +663,9 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     check_launch("k_sytrd");
     hipLaunchKernelGGL(k_stebz_stein, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
     check_launch("k_stebz_stein");
-    if (n <= 128) hipLaunchKernelGGL((k_ormtr<8>), dim3((kk + 15) / 16), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
-    else hipLaunchKernelGGL((k_ormtr<16>), dim3((kk + 15) / 16), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    if (n <= 64) hipLaunchKernelGGL((k_ormtr<1>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    else if (n <= 128) hipLaunchKernelGGL((k_ormtr<2>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    else hipLaunchKernelGGL((k_ormtr<4>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     check_launch("k_ormtr");
     if (stp) {   // per-phase cycles of the first steps: (b)-wait, reflector, wait, symv, wait, update (+ column)
         std::vector<unsigned long long> hst(768);
