@@ -1,6 +1,6 @@
 # round-3 records: full GPU suite, smoke, default bench line, rocprof kernel stats of it, PMC traffic passes
 set -o pipefail
-D=gpurun_out/r03p
+D=${D:-gpurun_out/r03p}
 mkdir -p $D
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 480 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests > $D/tests.log 2>&1
