@@ -599,7 +599,6 @@ __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, con
         __syncthreads();
         for (int e = threadIdx.x; e < (hi - lo + 1) * n; e += 256) sv[e] = V[size_t(lo) * n + e];
         __syncthreads();
-#pragma unroll 2
         for (int j = hi; j >= lo; --j) {   // (tau_j = 0: f = 0, z unchanged)
             const double* v = sv + size_t(j - lo) * n;
             double vv[ZE];
