@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "smallla.hpp"
@@ -211,12 +212,23 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
 #pragma unroll
         for (int i = lane; i < NP; i += 64) sk = fma(ps[i], vs[i], sk);
         const double K = -0.5 * tj * sum64(sk);
-        // (e) A -= v w^T + w v^T (v, w vanish at indices <= j: finished rows and columns stay untouched)
+        // (e) A -= v w^T + w v^T (v, w vanish at indices <= j: finished rows and columns stay untouched), on
+        //     the active blocks only: block rows / columns below (j + 1) / GRID are finished, so one
+        //     compile-time loop nest per first active block (a switch, not per-block branches)
+        auto update_from = [&](auto jb_c) {
+            constexpr int JB = decltype(jb_c)::value;
 #pragma unroll
-        for (int ib = 0; ib < NB; ++ib) {
-            const double wc = fma(K, vc[ib], pc[ib]);
+            for (int ib = JB; ib < NB; ++ib) {
+                const double wc = fma(K, vc[ib], pc[ib]);
 #pragma unroll
-            for (int ia = 0; ia < NB; ++ia) a[ia][ib] = fma(-vr[ia], wc, fma(-fma(K, vr[ia], pr[ia]), vc[ib], a[ia][ib]));
+                for (int ia = JB; ia < NB; ++ia) a[ia][ib] = fma(-vr[ia], wc, fma(-fma(K, vr[ia], pr[ia]), vc[ib], a[ia][ib]));
+            }
+        };
+        switch ((j + 1) / GRID) {
+            case 0: update_from(std::integral_constant<int, 0>{}); break;
+            case 1: if constexpr (NB > 1) update_from(std::integral_constant<int, (NB > 1 ? 1 : 0)>{}); break;
+            case 2: if constexpr (NB > 2) update_from(std::integral_constant<int, (NB > 2 ? 2 : 0)>{}); break;
+            default: if constexpr (NB > 3) update_from(std::integral_constant<int, (NB > 3 ? 3 : 0)>{}); break;
         }
         publish_column(j + 1);
     }
