@@ -70,6 +70,14 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+template <int NEWTON>
+__device__ __forceinline__ double rcpn(double x) {   // 1/x: hardware estimate + NEWTON Newton steps
+    double r = __builtin_amdgcn_rcp(x);
+#pragma unroll
+    for (int it = 0; it < NEWTON; ++it) r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+}
+
 __device__ __forceinline__ double rcp2(double x) {   // 1/x to ~1 ulp (hardware estimate + 2 Newton steps)
     double r = __builtin_amdgcn_rcp(x);
     double t = fma(-x, r, 1.0);
@@ -440,6 +448,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 // one 64-lane workgroup per wanted eigenvalue: block q -> the q-th largest (ascending index n - 1 - q).
 // Zt (kk x ldz): row q = the eigenvector of T (normalised); lam[q]. status[0] <- -1 if a multisection
 // did not reach full precision.
+template <int NEWTON>
 __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
                                                      double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status) {
     __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX];
@@ -478,7 +487,7 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         if (fabs(qv) < pivmin) qv = -pivmin;
         int c = qv < 0.0;
         for (int i = 1; i < n; ++i) {
-            qv = (sd[i] - x) - se2[i - 1] * rcp2(qv);
+            qv = (sd[i] - x) - se2[i - 1] * rcpn<NEWTON>(qv);
             if (fabs(qv) < pivmin) qv = -pivmin;
             c += qv < 0.0;
         }
@@ -510,12 +519,12 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         for (int i = 0; i + 1 < n; ++i) {
             if (fabs(ld[i]) >= fabs(ldl[i])) {
                 if (ld[i] != 0.0) {
-                    const double f = ldl[i] * rcp2(ld[i]);
+                    const double f = ldl[i] * rcpn<NEWTON>(ld[i]);
                     ldl[i] = f;
                     ld[i + 1] -= f * ldu[i];
                 }
             } else {
-                const double f = ld[i] * rcp2(ldl[i]);
+                const double f = ld[i] * rcpn<NEWTON>(ldl[i]);
                 ld[i] = ldl[i];
                 ldl[i] = f;
                 const double tmp = ldu[i];
@@ -672,7 +681,10 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
         hipLaunchKernelGGL(k_sytrd_l512, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
     }
     check_launch("k_sytrd");
-    hipLaunchKernelGGL(k_stebz_stein, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
+    // the chains' reciprocals: 2 Newton steps after the hardware estimate; XRS_SYEV_RCP1=1: one (A/B)
+    static const bool rcp1 = std::getenv("XRS_SYEV_RCP1") != nullptr;
+    if (rcp1) hipLaunchKernelGGL(k_stebz_stein<1>, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
+    else hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
     check_launch("k_stebz_stein");
     if (n <= 64) hipLaunchKernelGGL((k_ormtr<1>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     else if (n <= 128) hipLaunchKernelGGL((k_ormtr<2>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
