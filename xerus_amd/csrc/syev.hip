@@ -4,9 +4,10 @@
 // (tt_trunc.hip round_truncate), the kept left singular vectors of B are the eigenvectors of P's kk
 // largest eigenvalues. Three launches, LAPACK's dsytrd / dstebz / dstein / dormtr structure:
 //   1. k_sytrd: Householder tridiagonalisation A = Q T Q^T in ONE workgroup, the matrix register-resident
-//      (1024 threads on a 32 x 32 grid, element (i, k) on thread (i mod 32, k mod 32): the shrinking trailing
-//      block stays spread over every thread). Per column: the reflector from one wave, the symmetric
-//      matrix-vector product with in-half-wave reductions, the rank-2 update in registers -- 4 barriers.
+//      (n <= 128: 1024 threads on a 32 x 32 grid, element (i, k) on thread (i mod 32, k mod 32): the
+//      shrinking trailing block stays spread over every thread; 129..256: k_sytrd_l512, 512 threads holding
+//      the lower block triangle). Per column: the reflector from one wave, the symmetric matrix-vector
+//      product with in-wave DPP / permlane reductions, the rank-2 update in registers -- LDS-only barriers.
 //   2. k_stebz_stein: one wave per wanted eigenvalue (kk workgroups in parallel): Sturm-count
 //      multisection on 64 points per round (~9 rounds to full precision), then inverse iteration with the
 //      partially pivoted LU of T - lambda I (dgttrf / dgttrs), three solves from a fixed start vector.
