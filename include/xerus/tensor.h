@@ -128,6 +128,8 @@ class Tensor {
     std::string to_string() const;
 
     static size_t multiIndex_to_position(const MultiIndex& _multiIndex, const DimensionTuple& _dimensions);
+    /// the inverse (row-major, last index fastest): tensor.cpp position_to_multiIndex
+    static MultiIndex position_to_multiIndex(size_t _position, const DimensionTuple& _dimensions);
 
     void ensure_own_data();
     void apply_factor();
@@ -171,6 +173,8 @@ Tensor operator-(Tensor _lhs, const Tensor& _rhs);
 Tensor operator*(const value_t _factor, Tensor _tensor);
 Tensor operator*(Tensor _tensor, const value_t _factor);
 Tensor operator/(Tensor _tensor, const value_t _divisor);
+/// entrywise (Hadamard) product of equal-dimension tensors (tensor.cpp:1708-1740), one device kernel
+Tensor entrywise_product(const Tensor& _A, const Tensor& _B);
 
 inline value_t frob_norm(const Tensor& _tensor) { return _tensor.frob_norm(); }
 

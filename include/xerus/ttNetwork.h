@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "tensor.h"
+#include "tensorNetwork.h"
 
 namespace xerus {
 
@@ -61,6 +62,12 @@ class TTTensor {
     static std::vector<size_t> reduce_to_maximal_ranks(std::vector<size_t> _ranks, const std::vector<size_t>& _dimensions);
     /// all-ones rank-1 TT, then canonicalize_left (ttNetwork.cpp:170-191)
     static TTTensor ones(const std::vector<size_t>& _dimensions);
+    /// the Kronecker delta (1 where all indices are equal): cores are delta tensors of rank min(dims), then
+    /// canonicalize_left (ttNetwork.cpp:224-254)
+    static TTTensor kronecker(const std::vector<size_t>& _dimensions);
+    /// rank-1 unit tensor at _position (ttNetwork.cpp:257-283); not canonical for d >= 2
+    static TTTensor dirac(std::vector<size_t> _dimensions, const std::vector<size_t>& _position);
+    static TTTensor dirac(std::vector<size_t> _dimensions, const size_t _position);
 
     size_t degree() const { return dimensions.size(); }
     std::vector<size_t> ranks() const;
@@ -85,6 +92,17 @@ class TTTensor {
     void soft_threshold(const double _tau, const bool _preventZero = false);
 
     value_t frob_norm() const;
+
+    /// fixes mode _mode to _slatePosition: the sliced core (a matrix) is contracted into its right
+    /// neighbour (the left one for the last mode), as TensorNetwork::fix_mode + contract_unconnected_subnetworks
+    /// (ttNetwork.cpp:432-435, 748-778, tensorNetwork.cpp:912-951)
+    void fix_mode(const size_t _mode, const size_t _slatePosition);
+    /// Tensor::resize_mode on the core holding _mode, then the reference's re-canonicalisation
+    /// (ttNetwork.cpp:438-446)
+    void resize_mode(const size_t _mode, const size_t _newDim, const size_t _cutPos = ~0ul);
+    /// the networks left and right of component _position, each with the cut rank as an extra external
+    /// index (last on the left, first on the right), ghost nodes as the reference's (ttNetwork.cpp:515-580)
+    std::pair<TensorNetwork, TensorNetwork> chop(const size_t _position) const;
 
     TTTensor& operator+=(const TTTensor& _other);
     TTTensor& operator-=(const TTTensor& _other);
@@ -114,6 +132,13 @@ inline value_t frob_norm(const TTTensor& _tt) { return _tt.frob_norm(); }
 /// <x, y> on the GPU (left-to-right zipper, no permutations)
 value_t dot(const TTTensor& _x, const TTTensor& _y);
 bool approx_equal(const TTTensor& _a, const TTTensor& _b, const value_t _eps = EPSILON);
+/// entrywise (Hadamard) product, rank r_A r_B (ttNetwork.cpp:1275-1309): one HBM-bound kernel per core
+/// (xrs_tt_entrywise_product); moved to A's core position when both inputs are canonical
+TTTensor entrywise_product(const TTTensor& _A, const TTTensor& _B);
+/// the tensor product of two TTs: components of _lhs, then of _rhs (ttNetwork.cpp:1319-1429)
+TTTensor dyadic_product(const TTTensor& _lhs, const TTTensor& _rhs);
+/// repeated dyadic_product, right to left (ttNetwork.cpp:1435-1445)
+TTTensor dyadic_product(const std::vector<TTTensor>& _tensors);
 
 /// Indexed TT, supporting the full contraction value_t(x(i&0) * y(i&0)) of the reference.
 template <>
@@ -188,6 +213,11 @@ class TTOperator {
     static TTOperator identity(const std::vector<size_t>& _dimensions);
     /// all-ones operator (ttNetwork.cpp:169-191)
     static TTOperator ones(const std::vector<size_t>& _dimensions);
+    /// Kronecker delta over all 2d indices (ttNetwork.cpp:224-254)
+    static TTOperator kronecker(const std::vector<size_t>& _dimensions);
+    /// rank-1 unit operator (ttNetwork.cpp:257-283)
+    static TTOperator dirac(std::vector<size_t> _dimensions, const std::vector<size_t>& _position);
+    static TTOperator dirac(std::vector<size_t> _dimensions, const size_t _position);
 
     size_t degree() const { return dimensions.size(); }
     std::vector<size_t> ranks() const;
@@ -207,6 +237,13 @@ class TTOperator {
     value_t frob_norm() const;
     /// swaps row and column modes (ttNetwork.h:443-448)
     void transpose();
+    /// not available for operators (ttNetwork.cpp:433: REQUIRE)
+    void fix_mode(const size_t _mode, const size_t _slatePosition);
+    /// row modes 0..d-1, column modes d..2d-1 (ttNetwork.cpp:438-446)
+    void resize_mode(const size_t _mode, const size_t _newDim, const size_t _cutPos = ~0ul);
+    /// left / right networks of component _position (externals: row modes, column modes, then the cut rank
+    /// on the left; the cut rank, row modes, column modes on the right; ttNetwork.cpp:515-580)
+    std::pair<TensorNetwork, TensorNetwork> chop(const size_t _position) const;
 
     TTOperator& operator+=(const TTOperator& _other);
     TTOperator& operator-=(const TTOperator& _other);
@@ -237,6 +274,9 @@ TTOperator operator*(const value_t _factor, TTOperator _op);
 TTOperator operator*(TTOperator _op, const value_t _factor);
 TTOperator operator/(TTOperator _op, const value_t _divisor);
 inline value_t frob_norm(const TTOperator& _op) { return _op.frob_norm(); }
+TTOperator entrywise_product(const TTOperator& _A, const TTOperator& _B);
+TTOperator dyadic_product(const TTOperator& _lhs, const TTOperator& _rhs);
+TTOperator dyadic_product(const std::vector<TTOperator>& _tensors);
 
 template <>
 class IndexedTensor<TTOperator> {

@@ -172,6 +172,14 @@ int xrs_tt_round(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, doub
  *  taus: d-1 thresholds, taus[0] for the LAST edge (the reference's loop order). Core ends at 0. */
 int xrs_tt_soft_threshold(xrs_handle_t handle, size_t d, const size_t* n, size_t* r, double** cores,
                           int canonicalized, size_t core_position, const double* taus);
+/** Entrywise (Hadamard) product of two TTs of equal mode sizes (entrywise_product, ttNetwork.cpp:1275-1309,
+ *  core by core as perform_component_product, :1209-1272): out[k] = (ra[k] rb[k], ext[k], ra[k+1] rb[k+1])
+ *  with out[k][(a,b), i, (a',b')] = A[k][a, i, a'] B[k][b, i, b'] (fused rank a major, b minor), alpha
+ *  multiplied into out[0]. ext[k] = n_k for TTTensor cores, n_k m_k for TTOperator cores. Output cores come
+ *  from the handle's pool (release with xrs_free); no canonicalisation (the reference then moves the core
+ *  to A's core position when both inputs are canonical). */
+int xrs_tt_entrywise_product(xrs_handle_t handle, size_t d, const size_t* ext, const size_t* ra, const double* const* A,
+                             const size_t* rb, const double* const* B, double alpha, double** out);
 /** TTOperator application, the core-wise contraction of a TTStack (ttStack.cpp:197-309, built by
  *  TTNetwork<true>::specialized_contraction_f, ttNetwork.cpp:886-967). Operator A: cores
  *  (ra[k], n[k], m[k], ra[k+1]). With p == NULL, B is a TTTensor with cores (rb[k], m[k], rb[k+1]) and

@@ -1,0 +1,82 @@
+"""Subprocess body of tests/test_switches_gpu.py: a fixed set of GPU computations run under the environment
+switch being tested (the library reads its XRS_* switches once per process). Prints one JSON line of
+results (errors against numpy / the oracle, round paths, <x,y> values); test infrastructure only."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from oracle import xerus_ref as ref  # noqa: E402
+from ttutil import tt_diff_norm  # noqa: E402
+from xerus_amd import capi  # noqa: E402
+
+
+def main():
+    h = capi.Handle(0)
+    out = {}
+    rng = np.random.default_rng(7)
+    # GEMMs: a TT-chain shape (LDS-DMA pipeline eligible) and an odd shape (general kernel)
+    errs = []
+    for (m, n, k) in ((256, 5120, 256), (300, 170, 1000)):
+        A, B = rng.standard_normal((m, k)), rng.standard_normal((k, n))
+        dA, dB, dC = h.array(A), h.array(B), h.empty((m, n))
+        h.gemm(dC, m, n, 1.0, dA, k, False, k, dB, n, False)
+        E = A @ B
+        errs.append(float(np.abs(dC.numpy() - E).max() / np.abs(E).max()))
+    out["gemm_err"] = max(errs)
+    # <x,y> synchronous and asynchronous (the gate)
+    dims, ranks = [10] * 6, [10, 40, 40, 40, 10]
+    x = ref.TT.random_raw(dims, ranks, ref.Rng(3))
+    y = ref.TT.random_raw(dims, ranks, ref.Rng(4))
+    gx, gy = capi.TTDevice.from_cores(h, x.cores), capi.TTDevice.from_cores(h, y.cores)
+    nxy = np.sqrt(ref.dot(x, x) * ref.dot(y, y))
+    d_ref = ref.dot(x, y)
+    out["dot_err"] = abs(gx.dot(gy) - d_ref) / nxy
+    out["dot_async_err"] = abs(gx.dot_async(gy).result() - d_ref) / nxy
+    # non-truncating round (the certified chain)
+    gc = capi.TTDevice.from_cores(h, x.cores)
+    gc.round(40)
+    out["chain_path"] = h.last_round_path()
+    e, nrm = tt_diff_norm(gc.cores(), x.cores)
+    out["chain_err"] = e / nrm
+    # truncating round of a random TT (certified truncation) and of a graded one (general path)
+    xt = ref.TT.random(dims, ranks, ref.Rng(5))
+    g = capi.TTDevice.from_cores(h, xt.cores, canonicalized=True, core_position=0)
+    g.round(17)
+    out["trunc_path"] = h.last_round_path()
+    o = xt.copy()
+    o.round(17)
+    e_gpu, nrm = tt_diff_norm(g.cores(), xt.cores)
+    e_ref, _ = tt_diff_norm(o.cores, xt.cores)
+    out["trunc_ranks_ok"] = g.ranks == o.ranks
+    out["trunc_err_diff"] = abs(e_gpu - e_ref) / nrm
+    xg = ref.TT.random_raw(dims, ranks, ref.Rng(6))
+    for k in range(len(dims) - 1):
+        xg.cores[k] = xg.cores[k] * (0.7 ** np.arange(xg.cores[k].shape[2]))[None, None, :]
+    gg = capi.TTDevice.from_cores(h, [c.copy() for c in xg.cores])
+    gg.round(12)
+    out["graded_path"] = h.last_round_path()
+    og = xg.copy()
+    og.round(12)
+    e_gpu, nrm = tt_diff_norm(gg.cores(), xg.cores)
+    e_ref, _ = tt_diff_norm(og.cores, xg.cores)
+    out["graded_ranks_ok"] = gg.ranks == og.ranks
+    out["graded_err_diff"] = abs(e_gpu - e_ref) / nrm
+    # the block Jacobi right singular vectors (xrs_svd_rows_vt) and the eigensolver entry (xrs_sym_eig_top)
+    W = rng.standard_normal((64, 96))
+    S, Vt, sweeps = h.svd_rows_vt(h.array(W))
+    out["svd_err"] = float(np.abs(S.numpy() - np.linalg.svd(W, compute_uv=False)).max() / np.linalg.norm(W, 2))
+    P = W @ W.T
+    lam, Ut, st = h.sym_eig_top(h.array(P), 8)
+    out["eig_err"] = float(np.abs(lam.numpy() - np.linalg.eigvalsh(P)[::-1][:8]).max() / np.linalg.norm(P, 2))
+    h.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

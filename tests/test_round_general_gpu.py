@@ -102,3 +102,37 @@ def test_reference_path_ranks_above_512(handle, ref):
     block Jacobi); same ranks and truncation error as the oracle."""
     x = graded_tt(ref, [30, 30, 30, 30], [600, 600, 600], decay=0.97, seed=121)
     _check(handle, ref, x, [400] * 3, EPSILON, ("reference", "truncate"))
+
+
+def direct_sum_tt(ref, x, xp):
+    """z = x (+) x' as a TT: every mode index doubled, z = x on the first halves, x' on the second halves,
+    0 elsewhere; block-diagonal cores, so every edge unfolding is blockdiag(X_k, X'_k) and its singular
+    values are the union of x's and x''s (each one twice for x' = x)."""
+    d = x.order if hasattr(x, "order") else len(x.cores)
+    cores = []
+    for k in range(d):
+        A, B = x.cores[k], xp.cores[k]
+        a, n, b = A.shape
+        a2, n2, b2 = B.shape
+        ra = 1 if k == 0 else a + a2
+        rb = 1 if k == d - 1 else b + b2
+        Z = np.zeros((ra, n + n2, rb))
+        Z[:a, :n, :b] = A
+        Z[ra - a2:, n:, rb - b2:] = B
+        cores.append(Z)
+    return ref.TT(cores)
+
+
+@pytest.mark.parametrize("scale,target", [(1.0, 8), (1.0, 10), (1.0 + 1e-9, 7), (1.0 + 1e-9, 10)])
+def test_clustered_edge_spectra(handle, ref, scale, target):
+    """Every edge Gram with eigenvalues in exact (scale 1) or close (1e-9 apart) pairs: z = x (+) s x. The
+    exact pairs are kept or cut whole (even targets: the kept subspace is unique); the close pairs are also
+    cut between their members. Inverse iteration inside a cluster must keep its vectors orthogonal. Same
+    ranks and truncation error as the oracle, right-orthonormal cores to 1e-10, whichever path runs."""
+    x = ref.TT.random([6] * 6, [6] * 5, ref.Rng(131))
+    xs = x.copy()
+    xs.cores[0] = xs.cores[0] * scale
+    z = direct_sum_tt(ref, x, xs)
+    assert z.ranks == [12] * 5
+    _, _, path = _check(handle, ref, z, [target] * 5, EPSILON, ("truncate", "general", "reference"))
+    print(f"clustered spectra scale {scale} target {target}: path {path}")

@@ -361,38 +361,6 @@ def test_round_ranks_above_512(handle, ref, n, ranks):
     assert abs(e_gpu - e_ref) <= 1e-6 * nrm
 
 
-def test_paired_chain_launches(handle, ref, monkeypatch):
-    """XRS_GEMM_PAIR=1: both chains of the round and both ends of <x,y> as paired launches (k_gemm_glds2,
-    two shapes / transposes per grid) -- same results as the two-stream form within rounding."""
-    dims, ranks = [20] * 7, [20, 256, 256, 256, 256, 20]
-    rng = ref.Rng(21)
-    x = ref.TT.random_raw(dims, ranks, rng)
-    y = ref.TT.random_raw(dims, ranks, rng)
-    nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
-    d_ref = ref.dot(x, y)
-    ox = x.copy()
-    ox.move_core(0)
-    ox.round(256)
-    results = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("XRS_GEMM_PAIR", mode)
-        gx = capi.TTDevice.from_cores(handle, x.cores)
-        gy = capi.TTDevice.from_cores(handle, y.cores)
-        d = gx.dot(gy)
-        assert abs(d - d_ref) <= 1e-12 * nx * ny
-        assert abs(gx.dot_async(gy).result() - d_ref) <= 1e-12 * nx * ny
-        gx.move_core(0)
-        gx.round(256)
-        assert handle.last_round_path() == "chain"
-        assert gx.r == [1] + list(ox.ranks) + [1]
-        diff, nrm = _tt_diff_norm(ref, gx.cores(), ox.cores)
-        assert diff <= 1e-10 * nrm
-        results[mode] = d
-        gx.free()
-        gy.free()
-    assert abs(results["0"] - results["1"]) <= 1e-13 * nx * ny
-
-
 @pytest.mark.parametrize("edge", [None, 1])
 def test_dot_async_beside_fallback_round(handle, ref, edge):
     """x.dot_async(y) before a round whose first certificate fails (x + x: doubled ranks; or a

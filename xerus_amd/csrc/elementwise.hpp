@@ -37,8 +37,7 @@ void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t M, size_t 
 void gemm_sym(xrs_handle_t h, double* C, size_t N, double alpha, const double* A, size_t lda, bool ta, size_t K,
               const double* B, size_t ldb, bool tb);
 
-// Two independent GEMMs C_i = op(A_i) op(B_i) (alpha 1) as ONE launch when their shapes / transposes
-// allow (gemm.hip); false = nothing launched. sym: both results symmetric (lower tiles, mirrored).
+// One GEMM C = op(A) op(B) (alpha 1) as a value (planned ahead of its launch).
 struct GemmSpec {
     const double* A;
     const double* B;
@@ -46,8 +45,6 @@ struct GemmSpec {
     size_t M, N, K, lda, ldb;
     bool ta, tb;
 };
-// dry: only report whether the pair would be taken.
-bool gemm_pair(xrs_handle_t h, const GemmSpec& g0, const GemmSpec& g1, bool sym = false, bool dry = false);
 inline void gemm(xrs_handle_t h, const GemmSpec& g) {
     gemm(h, g.C, g.M, g.N, 1.0, g.A, g.lda, g.ta, g.K, g.B, g.ldb, g.tb);
 }

@@ -474,8 +474,7 @@ template <int BM, int BN, int BK = kGldsBK, int ST = 0>
 constexpr int glds_lds_doubles() { return glds_stages<BK, ST>() * (BM + BN) * BK; }
 
 // One output tile of the glds pipeline for entry blockIdx.y of `ptrs` (tile blockIdx.x, K-slice
-// blockIdx.z); `lds` holds glds_lds_doubles<BM, BN>() doubles. Shared by k_gemm_glds (one shape per
-// launch) and k_gemm_glds2 (two entries of different shapes / transposes in one launch).
+// blockIdx.z); `lds` holds glds_lds_doubles<BM, BN>() doubles (k_gemm_glds).
 template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK, int ST = 0>
 __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& ptrs, size_t lda, size_t ldb, int M, int N,
                                           int K, int kps, double alpha, double* __restrict__ slab, int tiles_m,
@@ -637,37 +636,6 @@ k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps
     XRS_TRACE_END
 }
 
-// Two GEMMs of different shapes and transposes in ONE launch (blockIdx.y = entry, each entry with its own
-// tile configuration; both configurations have the same wave count and the same number of tiles): the
-// two concurrent chains of a TT round / inner product step as one grid instead of two kernels sharing
-// the chip from two streams.
-struct GemmPair {
-    const double* A[2];
-    const double* B[2];
-    double* C[2];
-    size_t lda[2], ldb[2];
-    int M[2], N[2], tiles_m[2], xg[2];
-    __host__ __device__ const double* a(int i) const { return A[i]; }
-    __host__ __device__ const double* b(int i) const { return B[i]; }
-    __device__ double* c(int i) const { return C[i]; }
-};
-
-template <int BM0, int BN0, int WGM0, int WGN0, int WGK0, bool TA0, bool TB0,
-          int BM1, int BN1, int WGM1, int WGN1, int WGK1, bool TA1, bool TB1>
-__global__ void __launch_bounds__(WGM0 * WGN0 * WGK0 * 64, (glds_min_waves<BM0, BN0, WGM0, WGN0, WGK0>()))
-k_gemm_glds2(const GemmPair P, int K, int kps, double alpha, double* __restrict__ slab, int* __restrict__ tickets,
-             int sym) {
-    static_assert(WGM0 * WGN0 * WGK0 == WGM1 * WGN1 * WGK1, "both entries need the same wave count");
-    constexpr int L0 = glds_lds_doubles<BM0, BN0>(), L1 = glds_lds_doubles<BM1, BN1>();
-    __shared__ double lds[L0 > L1 ? L0 : L1];
-    if (blockIdx.y == 0)
-        glds_body<BM0, BN0, WGM0, WGN0, WGK0, TA0, TB0, GemmPair>(lds, P, P.lda[0], P.ldb[0], P.M[0], P.N[0], K, kps, alpha,
-                                                                slab, P.tiles_m[0], P.xg[0], tickets, sym, 0);
-    else
-        glds_body<BM1, BN1, WGM1, WGN1, WGK1, TA1, TB1, GemmPair>(lds, P, P.lda[1], P.ldb[1], P.M[1], P.N[1], K, kps, alpha,
-                                                                slab, P.tiles_m[1], P.xg[1], tickets, sym, 0);
-}
-
 template <class PTR>
 __global__ void __launch_bounds__(256) k_splitk_reduce(const PTR ptrs, const double* __restrict__ slab, size_t MN,
                                                        int splits, double alpha, int symN) {
@@ -707,8 +675,6 @@ static void launch_tiles(xrs_handle_t h, const PTR& P, int count, size_t lda, bo
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
-    static const bool noxcd = std::getenv("XRS_GEMM_NOXCD") != nullptr;
-    if (noxcd) xg = 0;
     KernelTimer timer(h, XRS_KFAM_GEMM, count * 2.0 * double(M) * double(N) * double(K),
                       count * 8.0 * (double(M) * K + double(K) * N + double(M) * N * splits));
 #define XRS_GEMM_LAUNCH(TA_, TB_)                                                                             \
@@ -792,12 +758,7 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         // 19.4; Grams 256^2 x 5120 g4 22.3-23.7, g3 23.4-25.2, g11 24.3-24.6 (old 25.5-28.0); 512x10240x512
         // and 512^2 x 10240: g4 117.8-125 (old 126-128)
         var = 0;
-        static const int sym_var = [] {   // XRS_GLDS_SYM_VAR: tile variant of symmetric Grams (experiments)
-            const char* e = std::getenv("XRS_GLDS_SYM_VAR");
-            return e ? std::atoi(e) : 0;
-        }();
-        if (sym && sym_var > 0 && sym_var <= 11 && fits(sym_var)) var = sym_var;
-        else if (sym) {
+        if (sym) {
             if (fits(4)) var = 4;
             else if (fits(5)) var = 5;
         } else if (fits(6) && ntiles(6) >= 192) var = 6;
@@ -807,20 +768,13 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         if (var == 0) return false;
     }
     if (var < 1 || var > 11 || !fits(var)) return false;
-    // 64-deep K-steps in 2 stages for the 8-wave tiles (XRS_GLDS_BK=64: experiment)
-    static const int bk_pref = [] {
-        const char* e = std::getenv("XRS_GLDS_BK");
-        return e ? std::atoi(e) : 32;
-    }();
-    const int bk = (bk_pref == 64 && K % 64 == 0 && (var == 4 || var == 6 || var == 7)) ? 64 : kGldsBK;
+    // (64-deep K-steps in 2 stages measured no faster: 18.5 vs 18.7 us on 256 x 5120 x 256)
+    const int bk = kGldsBK;
     // split-K: whole K-steps per slice, aiming at `target` workgroups
     const long tiles = ntiles(var);
     const int ksteps = K / bk;
     int splits = 1;
-    static const bool split_old = std::getenv("XRS_GLDS_SPLIT_OLD") != nullptr;   // (A/B: the plain target rule)
-    if (tiles < g_target && split_old) {
-        splits = int(std::min<long>((g_target + tiles - 1) / tiles, std::max(1, ksteps * bk / 128)));
-    } else if (tiles < g_target) {
+    if (tiles < g_target) {
         // Whole waves of workgroups: the launch takes rounds(s) x ceil(ksteps / s) K-steps per CU, where
         // rounds(s) = ceil(tiles s / resident) and resident = target x the workgroups one CU holds (LDS
         // stages of 96-128 KB: one; the 32x32 tile: three). Picking s by the target alone overshoots into a
@@ -849,9 +803,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
         case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
         case 3: XRS_GLDS(64, 64, 2, 2, 1); break;
-        case 4: if (bk == 64) XRS_GLDS(64, 64, 2, 2, 2, 64); else XRS_GLDS(64, 64, 2, 2, 2); break;
-        case 6: if (bk == 64) XRS_GLDS(64, 80, 4, 1, 2, 64); else XRS_GLDS(64, 80, 4, 1, 2); break;
-        case 7: if (bk == 64) XRS_GLDS(80, 64, 1, 4, 2, 64); else XRS_GLDS(80, 64, 1, 4, 2); break;
+        case 4: XRS_GLDS(64, 64, 2, 2, 2); break;
+        case 6: XRS_GLDS(64, 80, 4, 1, 2); break;
+        case 7: XRS_GLDS(80, 64, 1, 4, 2); break;
         case 8: XRS_GLDS(64, 80, 2, 1, 2); break;
         case 9: XRS_GLDS(80, 64, 1, 2, 2); break;
         case 10: XRS_GLDS(64, 64, 1, 1, 4); break;
@@ -897,22 +851,15 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
               bns[16] = {0, 128, 64, 32, 32, 32, 64, 64, 32, 32, 32, 32, 32, 32, 80, 64};
     int var = cfg_var;
     long cfg_target_eff = cfg_target;
-    static const long sym_target = [] {
-        const char* e = std::getenv("XRS_GEMM_SYM_TARGET");
-        return e ? std::atol(e) : 160L;   // measured: 160 -> 1.367 ms/step, 384 -> 1.390, 512 -> 1.398, 256 -> 1.481
-    }();
-    if (sym) cfg_target_eff = sym_target;
+    // symmetric results aim at 160 workgroups (measured: 160 -> 1.367 ms/step, 384 -> 1.390, 512 -> 1.398,
+    // 256 -> 1.481)
+    if (sym) cfg_target_eff = 160;
     if (sym) {
         // symmetric result: square tiles only (32, 64, 128), counted over the lower triangle
         auto lower = [&](int b) { const long T = (M + b - 1) / b; return long(count) * T * (T + 1) / 2; };
         auto ntl = [&](int v) { return lower(bms[v]); };
-        static const int sym_var = [] {
-            const char* e = std::getenv("XRS_GEMM_SYM_VAR");   // tuning: force 1, 2 or 4
-            return e ? std::atoi(e) : 0;
-        }();
         var = 4;
-        if (sym_var == 1 || sym_var == 2 || sym_var == 4) var = sym_var;
-        else if (lower(128) >= 1000) var = 1;
+        if (lower(128) >= 1000) var = 1;
         else if (lower(64) >= 512) var = 2;   // (13 Grams of 512^2: 32x32 unsplit 943 us < 64x64 1165 us)
         else if (lower(32) < 512)
             for (int v : {1, 2, 4}) {
@@ -937,12 +884,10 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         else if (ntiles(64, 32) >= 256) var = 3;
         else if (ntiles(32, 32) >= 512) var = 4;
         else {
-            static const bool prefer_inlaunch = std::getenv("XRS_GEMM_PREFER_INLAUNCH") != nullptr;
             var = 4;
             for (int v : {1, 2, 3}) {
                 const long t = ntiles(bms[v], bns[v]);
                 const long sp = std::min<long>((cfg_target_eff + t - 1) / t, std::max<long>(1, K / cfg_kmin));
-                if (prefer_inlaunch && sp * bms[v] * bns[v] * 8 > 65536) continue;
                 if (t * sp >= cfg_target_eff) { var = v; break; }
             }
         }
@@ -962,17 +907,11 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
     if (std::is_same<PTR, GemmMany>::value && var >= 5 && var <= 13) var = (var == 5 || var == 8 || var == 13) ? 3 : ((var == 9 || var >= 10) ? 4 : 2);   // tuning-only tiles: single GEMMs
     DevBuf slab;
     if (splits > 1) slab = DevBuf(h, size_t(count) * splits * M * N * sizeof(double));
-    // one-launch split-K when the tile grid fits the stream's ticket array (XRS_GEMM_SPLITK2=1: old
-    // two-kernel form, for A/B timing)
-    static const bool two_kernel = std::getenv("XRS_GEMM_SPLITK2") != nullptr;
-    // The last arriver reads splits x BM x BN doubles serially: worth it for small tiles only (the guide's
-    // "a few tens of KB" per tile; 128x128 tiles at 2 splits measured 70 us slower than the reduce kernel).
-    static const size_t slab_cap = [] {
-        const char* e = std::getenv("XRS_GEMM_SLAB_CAP");   // bytes per tile (tuning experiments)
-        return e ? size_t(std::atoll(e)) : size_t(65536);
-    }();
-    const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= slab_cap && bms[var] * bns[var] <= 4096;
-    int* tickets = (splits > 1 && !two_kernel && small_slab && ntiles(bms[var], bns[var]) <= xrs_handle_s::kTicketCap)
+    // one-launch split-K when the tile grid fits the stream's ticket array. The last arriver reads splits x
+    // BM x BN doubles serially: worth it for small tiles only (the guide's "a few tens of KB" per tile;
+    // 128x128 tiles at 2 splits measured 70 us slower than the reduce kernel, larger slab caps 0.3 ms/step)
+    const bool small_slab = size_t(splits) * bms[var] * bns[var] * sizeof(double) <= 65536 && bms[var] * bns[var] <= 4096;
+    int* tickets = (splits > 1 && small_slab && ntiles(bms[var], bns[var]) <= xrs_handle_s::kTicketCap)
                        ? h->tickets : nullptr;
 #define XRS_TILES(...) launch_tiles<__VA_ARGS__>(h, P, count, lda, ta, ldb, tb, M, N, K, splits, kps, alpha, slab.d(), tickets, sym ? 1 : 0)
     switch (var) {
@@ -1044,103 +983,6 @@ void gemm_batched(xrs_handle_t h, int count, double* const* C, size_t Ms, size_t
         }
         gemm_impl(h, P, c, Ms, Ns, alpha, lda, ta, Ks, ldb, tb, sym, tri);
     }
-}
-
-// Two independent GEMMs in one k_gemm_glds2 launch (see GemmPair). Taken when both are glds-eligible
-// (whole 32-deep K-steps, 16-B aligned operands, even leading dimensions), share K (and the result
-// size when split-K applies), and their transposes and shapes match an instantiated configuration:
-//   (NN, NN) and (TN, NN): 64x80 / 80x64 tiles (the T = G M / M H products of the chains, 256 tiles each
-//   at r = 256, n = 20); (TN, NT): 64x64 tiles (the chains' Grams M^T T / M T^T, symmetric or not).
-// false: nothing launched (the caller runs the two GEMMs separately).
-bool gemm_pair(xrs_handle_t h, const GemmSpec& g0, const GemmSpec& g1, bool sym, bool dry) {
-    // opt-in (XRS_GEMM_PAIR=1, read per call): measured slower than the two chains on two streams, where
-    // one chain's split-K reduce and boundary products overlap the other chain's GEMMs
-    const char* on = std::getenv("XRS_GEMM_PAIR");
-    if (on == nullptr || on[0] == '0' || g0.K != g1.K || g0.K == 0 || g0.K % kGldsBK != 0) return false;
-    const GemmSpec* g[2] = {&g0, &g1};
-    for (const GemmSpec* e : g) {
-        if ((e->lda & 1) || (e->ldb & 1) || (reinterpret_cast<uintptr_t>(e->A) & 15) || (reinterpret_cast<uintptr_t>(e->B) & 15))
-            return false;
-        if (e->M >= (1u << 30) || e->N >= (1u << 30) || e->K >= (1u << 30)) return false;
-    }
-    const int K = int(g0.K);
-    auto fits = [&](const GemmSpec& e, int bm, int bn) { return e.M % bm == 0 && e.N % bn == 0; };
-    // configuration: 0 = 64x80 (4,1,2), 1 = 80x64 (1,4,2), 2 = 64x64 (2,2,2)
-    int cfg[2];
-    const int bms[3] = {64, 80, 64}, bns[3] = {80, 64, 64};
-    for (int i = 0; i < 2; ++i) {
-        const GemmSpec& e = *g[i];
-        if (sym) cfg[i] = (e.M == e.N && fits(e, 64, 64)) ? 2 : -1;
-        else if (!(g0.ta && !g0.tb && !g1.ta && g1.tb) && fits(e, 64, 80)) cfg[i] = 0;
-        else if (!(g0.ta && !g0.tb && !g1.ta && g1.tb) && fits(e, 80, 64)) cfg[i] = 1;
-        else cfg[i] = fits(e, 64, 64) ? 2 : -1;
-        if (cfg[i] < 0) return false;
-    }
-    auto tiles = [&](int i) -> long {
-        const long tm = long(g[i]->M) / bms[cfg[i]], tn = long(g[i]->N) / bns[cfg[i]];
-        return sym ? tm * (tm + 1) / 2 : tm * tn;
-    };
-    if (tiles(0) != tiles(1)) return false;
-    // instantiated transpose / configuration combinations
-    const bool nn_nn = !g0.ta && !g0.tb && !g1.ta && !g1.tb;
-    const bool tn_nn = g0.ta && !g0.tb && !g1.ta && !g1.tb;
-    const bool tn_nt = g0.ta && !g0.tb && !g1.ta && g1.tb;
-    int kind = -1;
-    if ((nn_nn || tn_nn) && cfg[0] == 0 && cfg[1] == 1) kind = nn_nn ? 0 : 1;
-    else if (tn_nt && cfg[0] == 2 && cfg[1] == 2) kind = 2;
-    if (kind < 0) return false;
-    // split-K toward 256 workgroups in all, whole 32-deep steps per slice
-    const long t = 2 * tiles(0);
-    const int ksteps = K / kGldsBK;
-    int splits = 1;
-    if (t < 256) splits = int(std::min<long>((256 + t - 1) / t, std::max(1, ksteps / 4)));
-    int kps = (ksteps + splits - 1) / splits * kGldsBK;
-    splits = (K + kps - 1) / kps;
-    if (splits > 1 && g0.M * g0.N != g1.M * g1.N) return false;   // (slab layout: equal result sizes)
-    if (dry) return true;
-    GemmPair P{};
-    for (int i = 0; i < 2; ++i) {
-        const GemmSpec& e = *g[i];
-        P.A[i] = e.A;
-        P.B[i] = e.B;
-        P.C[i] = e.C;
-        P.lda[i] = e.lda;
-        P.ldb[i] = e.ldb;
-        P.M[i] = int(e.M);
-        P.N[i] = int(e.N);
-        P.tiles_m[i] = int(e.M) / bms[cfg[i]];
-        const int tn = int(e.N) / bns[cfg[i]];
-        P.xg[i] = sym ? 0 : (e.N >= e.M ? ((tn % 8 == 0) ? 1 : 0) : ((P.tiles_m[i] % 8 == 0) ? 2 : 0));
-    }
-    const size_t MN = g0.M * g0.N;
-    DevBuf slab;
-    if (splits > 1) slab = DevBuf(h, 2 * size_t(splits) * MN * sizeof(double));
-    // in-launch combine for small per-tile slabs (as gemm_glds)
-    const bool small_slab = size_t(splits) * 64 * 64 * sizeof(double) <= 65536;
-    int* tickets = (splits > 1 && kind == 2 && small_slab && 2 * tiles(0) <= xrs_handle_s::kTicketCap) ? h->tickets : nullptr;
-    KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * (double(g0.M) * g0.N + double(g1.M) * g1.N) * K,
-                      8.0 * (double(g0.M) * K + double(K) * g0.N + double(g1.M) * K + double(K) * g1.N +
-                             (double(g0.M) * g0.N + double(g1.M) * g1.N) * splits));
-    const dim3 grid(unsigned(tiles(0)), 2u, unsigned(splits));
-    const int symf = sym ? 1 : 0;
-    if (kind == 0)
-        hipLaunchKernelGGL((k_gemm_glds2<64, 80, 4, 1, 2, false, false, 80, 64, 1, 4, 2, false, false>), grid, dim3(512), 0,
-                           h->stream, P, K, kps, 1.0, slab.d(), tickets, symf);
-    else if (kind == 1)
-        hipLaunchKernelGGL((k_gemm_glds2<64, 80, 4, 1, 2, true, false, 80, 64, 1, 4, 2, false, false>), grid, dim3(512), 0,
-                           h->stream, P, K, kps, 1.0, slab.d(), tickets, symf);
-    else
-        hipLaunchKernelGGL((k_gemm_glds2<64, 64, 2, 2, 2, true, false, 64, 64, 2, 2, 2, false, true>), grid, dim3(512), 0,
-                           h->stream, P, K, kps, 1.0, slab.d(), tickets, symf);
-    check_launch("k_gemm_glds2");
-    if (splits > 1 && tickets == nullptr) {
-        const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
-        KernelTimer t2(h, XRS_KFAM_ELEMWISE, 2.0 * double(MN) * splits, 2 * 8.0 * double(MN) * (splits + 1));
-        hipLaunchKernelGGL(k_splitk_reduce<GemmPair>, dim3(blocks, 2u), dim3(256), 0, h->stream, P, slab.d(), MN, splits,
-                           1.0, sym ? int(g0.N) : 0);
-        check_launch("k_splitk_reduce");
-    }
-    return true;
 }
 
 }  // namespace xrs

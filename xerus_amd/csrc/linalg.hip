@@ -443,16 +443,14 @@ static void svd_big(xrs_handle_t h, const double* A, size_t m, size_t n, double*
     orthogonalize(h, A, m, n, false, Q.d(), R.d());
     XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
     jacobi_vt(h, R.d(), int(n), false, int(n), int(n), S, Vt, int(n), st.as<int>(), 60);
+    jacobi_settle(h, st.as<int>(), int(n), int(n), [&](int kernel) {   // (-2: recomputed, see jacobi_settle)
+        jacobi_vt(h, R.d(), int(n), false, int(n), int(n), S, Vt, int(n), st.as<int>(), 60, kernel);
+    });
     gemm(h, Ur.d(), n, n, 1.0, R.d(), n, false, n, Vt, n, true);   // R V = U_R S
     hipLaunchKernelGGL(k_div_cols, dim3(unsigned(std::min<size_t>((n * n + 255) / 256, 4096))), dim3(256), 0, h->stream, Ur.d(), S, n, n);
     check_launch("k_div_cols");
     gemm(h, Uq.d(), m, n, 1.0, Q.d(), n, false, n, Ur.d(), n, false);   // Q U_R
     orthogonalize(h, Uq.d(), m, n, false, U, Rn.d());
-    int sw = 0;
-    read_status(h, st.as<int>(), 1, &sw);
-    if (sw < 0)
-        std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %zu x %zu matrix did not converge (status %d)\n", n, n,
-                     sw);
 }
 
 void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
@@ -545,11 +543,11 @@ int xrs_svd_rows_vt(xrs_handle_t h, double* S, double* Vt, int* sweeps, const do
                     "xrs_svd_rows_vt: need 1 <= p <= q <= 1024 (kernel 1: p <= 512)");
         DevBuf st(h, 64);
         XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
-        jacobi_vt(h, A, int(q), false, int(p), int(q), S, Vt, int(q), st.as<int>(), 40, kernel, std::getenv("XRS_SVD_TIMING") != nullptr);
+        jacobi_vt(h, A, int(q), false, int(p), int(q), S, Vt, int(q), st.as<int>(), 40, kernel, stamps_enabled("svd"));
         int sts[9];
         read_status(h, st.as<int>(), 9, sts);
         *sweeps = sts[0];
-        if (std::getenv("XRS_SVD_TIMING"))
+        if (stamps_enabled("svd"))
             std::fprintf(stderr, "jacobi_vt p=%zu q=%zu kernel=%d: sweeps %d, 100 MHz ticks: total %d, grid barriers %d, exchange %d; "
                          "thread-0 cross-round cycles: dot %d, rotation %d, update %d, barrier %d, rotations %d\n",
                          p, q, kernel, sts[0], sts[1], sts[2], sts[3], sts[4], sts[5], sts[6], sts[7], sts[8]);

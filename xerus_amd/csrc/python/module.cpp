@@ -256,6 +256,17 @@ PYBIND11_MODULE(xerus, m) {
     });
     m.def("file_type", &misc::file_type);
 
+    // ------------------------------------------------------------------ TensorNetwork (results of chop)
+    py::class_<TensorNetwork>(m, "TensorNetwork")
+        .def(py::init<>())
+        .def(py::init<Tensor>())
+        .def_readonly("dimensions", &TensorNetwork::dimensions)
+        .def("degree", &TensorNetwork::degree)
+        .def("num_nodes", &TensorNetwork::num_nodes)
+        .def("frob_norm", &TensorNetwork::frob_norm)
+        .def("to_tensor", &TensorNetwork::to_tensor)
+        .def("require_valid_network", &TensorNetwork::require_valid_network);
+
     // ------------------------------------------------------------------ TTTensor
     py::class_<IndexedTTStack>(m, "IndexedTTStack")
         .def("__mul__", [](const IndexedTTStack& _s, const IndexedTensor<TTTensor>& _y) { return _s * _y; });
@@ -284,6 +295,13 @@ PYBIND11_MODULE(xerus, m) {
                     [](const std::vector<size_t>& _dims, const std::vector<size_t>& _ranks) { return TTTensor::random_raw(_dims, _ranks); })
         .def_static("reduce_to_maximal_ranks", &TTTensor::reduce_to_maximal_ranks)
         .def_static("ones", &TTTensor::ones)
+        .def_static("kronecker", &TTTensor::kronecker)
+        .def_static("dirac", py::overload_cast<std::vector<size_t>, const std::vector<size_t>&>(&TTTensor::dirac))
+        .def_static("dirac", py::overload_cast<std::vector<size_t>, const size_t>(&TTTensor::dirac))
+        .def("fix_mode", &TTTensor::fix_mode)
+        .def("resize_mode", &TTTensor::resize_mode, py::arg("mode"), py::arg("newDim"), py::arg("cutPos") = ~0ul)
+        .def("chop", &TTTensor::chop)
+        .def("require_correct_format", &TTTensor::require_correct_format)
         .def_readonly("dimensions", &TTTensor::dimensions)
         .def_readonly("canonicalized", &TTTensor::canonicalized)
         .def_readonly("corePosition", &TTTensor::corePosition)
@@ -316,6 +334,14 @@ PYBIND11_MODULE(xerus, m) {
         .def(py::self / value_t())
         .def("__copy__", [](const TTTensor& _t) { return TTTensor(_t); });
     m.def("dot", [](const TTTensor& _x, const TTTensor& _y) { return dot(_x, _y); });
+    m.def("entrywise_product", py::overload_cast<const Tensor&, const Tensor&>(&entrywise_product));
+    m.def("entrywise_product", py::overload_cast<const TTTensor&, const TTTensor&>(&entrywise_product));
+    m.def("entrywise_product", py::overload_cast<const TTOperator&, const TTOperator&>(&entrywise_product));
+    m.def("dyadic_product", py::overload_cast<const TTTensor&, const TTTensor&>(&dyadic_product));
+    m.def("dyadic_product", py::overload_cast<const std::vector<TTTensor>&>(&dyadic_product));
+    m.def("dyadic_product", py::overload_cast<const TTOperator&, const TTOperator&>(&dyadic_product));
+    m.def("dyadic_product", py::overload_cast<const std::vector<TTOperator>&>(&dyadic_product));
+    m.def("position_to_multiIndex", &Tensor::position_to_multiIndex);
 
     // ------------------------------------------------------------------ ALS (algorithms/als.h)
     py::class_<ALSVariant>(m, "ALSVariant")
@@ -419,6 +445,13 @@ PYBIND11_MODULE(xerus, m) {
         .def_static("random", [](const std::vector<size_t>& _dims, size_t _rank) { return TTOperator::random(_dims, _rank); })
         .def_static("identity", &TTOperator::identity)
         .def_static("ones", &TTOperator::ones)
+        .def_static("kronecker", &TTOperator::kronecker)
+        .def_static("dirac", py::overload_cast<std::vector<size_t>, const std::vector<size_t>&>(&TTOperator::dirac))
+        .def_static("dirac", py::overload_cast<std::vector<size_t>, const size_t>(&TTOperator::dirac))
+        .def("fix_mode", &TTOperator::fix_mode)
+        .def("resize_mode", &TTOperator::resize_mode, py::arg("mode"), py::arg("newDim"), py::arg("cutPos") = ~0ul)
+        .def("chop", &TTOperator::chop)
+        .def("require_correct_format", &TTOperator::require_correct_format)
         .def_readonly("dimensions", &TTOperator::dimensions)
         .def_readonly("canonicalized", &TTOperator::canonicalized)
         .def_readonly("corePosition", &TTOperator::corePosition)

@@ -101,17 +101,7 @@ static int sync_debug() {
     return v;
 }
 
-void host_wait(xrs_handle_t h) {
-    static const bool spin = std::getenv("XRS_SYNC_SPIN") != nullptr;
-    if (!spin) {
-        XRS_HIP(hipStreamSynchronize(h->stream));
-        return;
-    }
-    XRS_HIP(hipEventRecord(h->ev_host, h->stream));
-    hipError_t e;
-    while ((e = hipEventQuery(h->ev_host)) == hipErrorNotReady) __builtin_ia32_pause();
-    XRS_HIP(e);
-}
+void host_wait(xrs_handle_t h) { XRS_HIP(hipStreamSynchronize(h->stream)); }
 
 void fence_readers(xrs_handle_t h) {
     if (!h->reader_pending) return;
@@ -120,6 +110,13 @@ void fence_readers(xrs_handle_t h) {
     // round releases x's old cores after its own check synchronisation)
     wait_dot_done(h);
     h->reader_pending = false;
+}
+
+bool stamps_enabled(const char* what) {
+    const char* e = std::getenv("XRS_STAMPS");
+    if (!e || !*e) return false;
+    const std::string list = std::string(",") + e + ",";
+    return list.find(",all,") != std::string::npos || list.find(std::string(",") + what + ",") != std::string::npos;
 }
 
 void check_launch(const char* what) {
@@ -144,41 +141,26 @@ extern "C" {
 const char* xrs_last_error(void) { return g_last_error.c_str(); }
 const char* xrs_version(void) { return "xerus_amd 0.1 (gfx950)"; }
 
-// Cross-stream dependencies: hipEventRecord + hipStreamWaitEvent. XRS_FORK_VALUES=1 selects stream
-// write-value / wait-value packets instead: one isolated hop measured 8.7 us vs 17.7 us
-// (tools/boundary_bench.hip), but the bench step did not get faster (1.46 vs 1.43 ms), so events stay.
-static bool fork_events() {
-    static const bool v = std::getenv("XRS_FORK_VALUES") == nullptr;
-    return v;
-}
-
-static void stream_signal(xrs_handle_t h, int word, hipStream_t producer, hipStream_t consumer, hipEvent_t ev) {
-    if (fork_events()) {
-        XRS_HIP(hipEventRecord(ev, producer));
-        XRS_HIP(hipStreamWaitEvent(consumer, ev, 0));
-        return;
-    }
-    const unsigned e = ++h->sync_epoch[word];
-    unsigned* w = h->sync_words + 16 * word;
-    XRS_HIP(hipStreamWriteValue32(producer, w, e, 0));
-    XRS_HIP(hipStreamWaitValue32(consumer, w, e, hipStreamWaitValueGte, 0xffffffffu));
+// Cross-stream dependencies: hipEventRecord + hipStreamWaitEvent. (Stream write-value / wait-value
+// packets measured 8.7 vs 17.7 us for one isolated hop, tools/boundary_bench.hip, but the bench step did not
+// get faster, 1.46 vs 1.43 ms, so events stay.)
+static void stream_signal(hipStream_t producer, hipStream_t consumer, hipEvent_t ev) {
+    XRS_HIP(hipEventRecord(ev, producer));
+    XRS_HIP(hipStreamWaitEvent(consumer, ev, 0));
 }
 
 StreamFork::StreamFork(xrs_handle_t h, int sides)
     : h_(h), sides_(std::max(1, std::min(sides, int(xrs_handle_s::kSides)))), main_stream_(h->stream), main_pool_(h->pool),
       main_tickets_(h->tickets) {
-    if (fork_events()) {
-        XRS_HIP(hipEventRecord(h_->ev_fork, main_stream_));
-        for (int i = 0; i < sides_; ++i) XRS_HIP(hipStreamWaitEvent(h_->side_stream[i], h_->ev_fork, 0));
-        return;
-    }
-    const unsigned e = ++h_->sync_epoch[0];
-    XRS_HIP(hipStreamWriteValue32(main_stream_, h_->sync_words, e, 0));
-    for (int i = 0; i < sides_; ++i)
-        XRS_HIP(hipStreamWaitValue32(h_->side_stream[i], h_->sync_words, e, hipStreamWaitValueGte, 0xffffffffu));
+    XRS_HIP(hipEventRecord(h_->ev_fork, main_stream_));
+    for (int i = 0; i < sides_; ++i) XRS_HIP(hipStreamWaitEvent(h_->side_stream[i], h_->ev_fork, 0));
 }
 
 void StreamFork::side(int i) {
+    // while kernels are being timed (xrs_prof_begin), the fork's lanes all stay on the main stream: every
+    // event pair then brackets exactly one kernel (with concurrent lanes it also spans the time a kernel
+    // waits for CUs held by the other lane's kernels), so the event durations agree with a kernel trace
+    if (h_->prof_mask) return;
     h_->stream = h_->side_stream[i];
     h_->pool = h_->side_pool[i];
     h_->tickets = h_->side_tickets[i];
@@ -199,7 +181,7 @@ void StreamFork::join() {
     if (joined_) return;
     joined_ = true;
     main();
-    for (int i = 0; i < sides_; ++i) stream_signal(h_, 1 + i, h_->side_stream[i], main_stream_, h_->ev_join[i]);
+    for (int i = 0; i < sides_; ++i) stream_signal(h_->side_stream[i], main_stream_, h_->ev_join[i]);
 }
 
 StreamFork::~StreamFork() {
@@ -224,15 +206,12 @@ int xrs_create(xrs_handle_t* handle, int device) {
         h->stream = h->own_stream;
         // side streams 1 and 2 carry the asynchronous inner product at the lowest queue priority, so the
         // work enqueued beside it (the round on the main stream) is dispatched first and the product
-        // fills the gaps (bench step 1.19 -> 1.16 ms). XRS_ASYNC_PRIORITY=normal|high for experiments.
+        // fills the gaps (bench step 1.19 -> 1.16 ms)
         int prio_least = 0, prio_greatest = 0;
         (void)hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest);
-        const char* ap = std::getenv("XRS_ASYNC_PRIORITY");
-        const bool ap_set = !(ap && std::strcmp(ap, "normal") == 0) && prio_least != prio_greatest;
-        const int async_prio = (ap && std::strcmp(ap, "high") == 0) ? prio_greatest : prio_least;
         for (int i = 0; i < xrs_handle_s::kSides; ++i) {
-            if (ap_set && i >= 1)
-                XRS_HIP(hipStreamCreateWithPriority(&h->side_stream[i], hipStreamNonBlocking, async_prio));
+            if (i >= 1 && prio_least != prio_greatest)
+                XRS_HIP(hipStreamCreateWithPriority(&h->side_stream[i], hipStreamNonBlocking, prio_least));
             else
                 XRS_HIP(hipStreamCreateWithFlags(&h->side_stream[i], hipStreamNonBlocking));
         }
@@ -271,20 +250,17 @@ static void init_handle_resources(xrs_handle_t h) {
         }
         XRS_HIP(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
         XRS_HIP(hipEventCreateWithFlags(&h->ev_aux, hipEventDisableTiming));
-        XRS_HIP(hipEventCreateWithFlags(&h->ev_host, hipEventDisableTiming));
         XRS_HIP(hipEventCreateWithFlags(&h->ev_dot, hipEventDisableTiming));
         XRS_HIP(hipEventCreateWithFlags(&h->ev_dot_join, hipEventDisableTiming));
         XRS_HIP(hipHostMalloc(&h->host_scratch, 1 << 16, hipHostMallocDefault));
         XRS_HIP(hipMalloc(&h->dev_scratch, 1 << 16));
         const size_t tbytes = size_t(1 + xrs_handle_s::kSides) * xrs_handle_s::kTicketCap * sizeof(int);
-        XRS_HIP(hipMalloc(&h->sync_words, 64 * (1 + xrs_handle_s::kSides)));
-        XRS_HIP(hipMemset(h->sync_words, 0, 64 * (1 + xrs_handle_s::kSides)));
         XRS_HIP(hipMalloc(&h->ticket_base, tbytes));
         XRS_HIP(hipMemset(h->ticket_base, 0, tbytes));
         h->tickets = h->ticket_base;
         for (int i = 0; i < xrs_handle_s::kSides; ++i)
             h->side_tickets[i] = h->ticket_base + size_t(1 + i) * xrs_handle_s::kTicketCap;
-        // the zeroed tickets / sync words must be in place before any (non-blocking) stream uses them
+        // the zeroed tickets must be in place before any (non-blocking) stream uses them
         XRS_HIP(hipDeviceSynchronize());
     }
 }
@@ -312,13 +288,11 @@ int xrs_destroy(xrs_handle_t h) {
         }
         if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
         if (h->ev_aux) (void)hipEventDestroy(h->ev_aux);
-        if (h->ev_host) (void)hipEventDestroy(h->ev_host);
         if (h->ev_dot) (void)hipEventDestroy(h->ev_dot);
         if (h->ev_dot_join) (void)hipEventDestroy(h->ev_dot_join);
         (void)hipHostFree(h->host_scratch);
         (void)hipFree(h->dev_scratch);
         (void)hipFree(h->ticket_base);
-        (void)hipFree(h->sync_words);
         if (h->own_stream && !h->borrowed_streams) (void)hipStreamDestroy(h->own_stream);
         delete h;
     });

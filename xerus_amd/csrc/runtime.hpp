@@ -99,11 +99,6 @@ struct xrs_handle_s {
     xrs::Pool* side_pool[kSides] = {};
     hipEvent_t ev_fork = nullptr, ev_join[kSides] = {};
     hipEvent_t ev_aux = nullptr;   // one extra cross-stream dependency inside a fork (see tt.hip chain_pass)
-    hipEvent_t ev_host = nullptr;  // host read-back point (host_wait)
-    // fork/join words for stream write-value / wait-value dependencies (one 64-byte line each: main, sides);
-    // epochs only grow (waits are >=)
-    unsigned* sync_words = nullptr;
-    unsigned sync_epoch[1 + kSides] = {};
     // split-K arrival tickets (zero between launches; the last arriving slice resets its word), one
     // array per stream so concurrent launches never share a word; `tickets` follows `stream`
     static constexpr int kTicketCap = 4096;
@@ -167,9 +162,26 @@ class KernelTimer {
 
 void check_launch(const char* what);
 
+// Diagnostic cycle / time stamps (stderr), off by default: XRS_STAMPS is a comma-separated list of
+// "round" (host phase marks of round()), "svd" (block Jacobi phase cycles of xrs_svd_rows_vt), "syev"
+// (tridiagonalisation column-step cycles), or "all".
+bool stamps_enabled(const char* what);
+
+// Runs the handle's launches on another stream for one scope (the main stream is restored on scope exit,
+// also when a launch throws). The caller orders the two streams (events).
+class StreamSwap {
+   public:
+    StreamSwap(xrs_handle_t h, hipStream_t s) : h_(h), saved_(h->stream) { h_->stream = s; }
+    ~StreamSwap() { h_->stream = saved_; }
+    StreamSwap(const StreamSwap&) = delete;
+    StreamSwap& operator=(const StreamSwap&) = delete;
+   private:
+    xrs_handle_t h_;
+    hipStream_t saved_;
+};
+
 // Host wait for everything enqueued on h->stream so far (the read-backs of a TT call: a scalar, the round's
-// check values). XRS_SYNC_SPIN=1 polls an event instead of hipStreamSynchronize (measured: no difference,
-// 1.3361 vs 1.3305 ms/step).
+// check values). (Polling an event instead measured no difference: 1.3361 vs 1.3305 ms/step.)
 void host_wait(xrs_handle_t h);
 
 // Order the current stream after an in-flight asynchronous reader of the handle's blocks (the async

@@ -1,5 +1,6 @@
 // Launch wrappers of the small dense kernels (smallla.hip) and the factorisation drivers (linalg.cpp).
 #pragma once
+#include <functional>
 #include <vector>
 
 #include "elementwise.hpp"
@@ -78,6 +79,12 @@ void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int
 // accumulated rotations on the rows of F^T, upper (R of B = Q R) on the rows of F. Enqueued only.
 void jacobi_right_vectors(xrs_handle_t h, const double* F, int g, bool lower, double* S, double* Vt, int* status_dev,
                           int max_sweeps = 40);
+
+// Reads a Jacobi status word (synchronises) and returns it. -2 (a grid-barrier poll of the block kernel timed
+// out) means the outputs are invalid, not a convergence failure: rerun(kernel) recomputes them (kernel 1 = one
+// workgroup where p <= 512, else the block kernel once more); a second -2 throws. Other negative statuses are
+// non-convergence warnings, as the reference's dgesdd failure (blasLapackWrapper.cpp:216-224).
+int jacobi_settle(xrs_handle_t h, int* status_dev, int p, int q, const std::function<void(int kernel)>& rerun);
 
 struct OrthResult {
     bool certified;   // sigma_min(A) >= cert_ratio * ||A||_F proven (Cholesky of the shifted Gram succeeded)

@@ -102,28 +102,6 @@ __device__ __forceinline__ void rotation(double a, double b, double c, double& s
     rotation(a, b, c, s, tau, tn);
 }
 
-// The same rotation with its angle from an FP32 estimate and an exactly consistent FP64 (s, tau):
-// tau = tan(theta/2) is rounded to FP32 (and then exact), s = 2 tau / (1 + tau^2) = sin(theta) to ~1 ulp,
-// so the applied transform [[1 - s tau, -s], [s, 1 - s tau]] is orthogonal to ~u whatever the angle's
-// accuracy. The angle is within ~1e-7 of the zeroing one: the pair's inner product drops by ~1e7 instead
-// of to zero, which the next sweeps absorb (the convergence test always uses fresh dot products). The
-// dependent chain is ~12 FP32 + ~8 FP64 operations instead of ~35 FP64 ones (three Newton-refined
-// FP64 reciprocals / square roots). Inputs are scaled to FP32 range by the exponent of max(|b - a|, |c|).
-// dn = the change of the first norm: a' = a + dn, b' = b - dn (a' = |x'|^2 for the applied angle).
-__device__ __forceinline__ void rotation_fast(double a, double b, double c, double& s, double& tau, double& dn) {
-    const double dd = b - a;
-    const double m = fmax(fabs(dd), fabs(c));
-    const int e = __builtin_amdgcn_frexp_exp(m);
-    const float ddf = float(__builtin_amdgcn_ldexp(dd, -e)), cf = float(__builtin_amdgcn_ldexp(c, -e));
-    const float h = __builtin_amdgcn_sqrtf(fmaf(ddf, ddf, 4.0f * cf * cf));
-    const float tf = copysignf(2.0f, ddf) * cf * __builtin_amdgcn_rcpf(fabsf(ddf) + h);   // tan(theta), |t| <= 1
-    const float tauf = tf * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_sqrtf(fmaf(tf, tf, 1.0f)));
-    tau = double(tauf);
-    s = 2.0 * tau * frcp(fma(tau, tau, 1.0));
-    const double cs = fma(-s, tau, 1.0);   // cos(theta)
-    dn = s * fma(s, dd, -2.0 * cs * c);    // sin^2 (b - a) - 2 sin cos c
-}
-
 // rows padded with zeros to E * G (no bounds checks: the padding stays zero under rotations)
 template <int G, int E>
 __device__ __forceinline__ void load_row_full(double (&x)[E], const double* __restrict__ w, int l) {
@@ -142,7 +120,7 @@ __device__ __forceinline__ void store_row_full(const double (&x)[E], double* __r
 // The register core: the lane's E elements of each row (zero beyond q, which rotations keep zero)
 // (the inner products run over the first ew elements: the rest may carry accumulated rotations)
 template <int G, int E>
-__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E, bool fast = false) {
+__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E) {
     double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -157,12 +135,7 @@ __device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], doub
     c = gsum<G>(c);
     if (!(c * c > tol2 * a * b)) return false;
     double s, tau;
-    if (fast) {
-        double dn;
-        rotation_fast(a, b, c, s, tau, dn);
-    } else {
-        rotation(a, b, c, s, tau);
-    }
+    rotation(a, b, c, s, tau);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const double xe = x[e], ye = y[e];
@@ -400,7 +373,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                                                                  double* __restrict__ S, double* __restrict__ Vt, int ldvt,
                                                                  double* __restrict__ U, int ldu, int* __restrict__ status, int flags) {
     constexpr int NT = BR * G, R2 = 2 * BR;
-    const bool stamps = (flags & 1) != 0, fast_rot = (flags & 2) != 0;
+    const bool stamps = (flags & 1) != 0;
     // diagnostics (stamps != 0, XRS_SVD_TIMING): cycles of thread 0 per cross-round phase -- dot + sum,
     // rotation parameters, update + store, barrier wait -- and the rotation count, into status[4..8]
     unsigned long long st_ph[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
@@ -457,7 +430,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                     double x[E], y[E];
                     load_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                     load_row_full<G, E>(y, Ws + (base + j) * ldw, l);
-                    if (rotate_regs<G, E>(x, y, tol2, ew, fast_rot)) {
+                    if (rotate_regs<G, E>(x, y, tol2, ew)) {
                         store_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                         store_row_full<G, E>(y, Ws + (base + j) * ldw, l);
                         if (l == 0) rotated = 1;
@@ -503,9 +476,8 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                         st_ph[0] += c1 - c0;
                     }
                     if (do_rot) {
-                        double sn, tau, tn = 0.0, dn = 0.0;
-                        if (fast_rot) rotation_fast(a, b, c, sn, tau, dn);
-                        else rotation(a, b, c, sn, tau, tn);
+                        double sn, tau, tn = 0.0;
+                        rotation(a, b, c, sn, tau, tn);
                         if (stamps) {
                             c2 = __builtin_amdgcn_s_memtime() + (sn != sn ? 1ull : 0ull);
                             st_ph[1] += c2 - c1;
@@ -517,7 +489,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                             x[e] = xe - sn * fma(tau, xe, ye);
                             y[e] = ye + sn * fma(-tau, ye, xe);
                         }
-                        double an = fast_rot ? a + dn : fma(-tn, c, a), bnew = fast_rot ? b - dn : fma(tn, c, b);
+                        double an = fma(-tn, c, a), bnew = fma(tn, c, b);
                         if (an < 0.5 * a) {
                             an = 0.0;
 #pragma unroll
@@ -625,18 +597,6 @@ bool jacobi_vt_fits_lds(int p, int q) { return q <= 128 && size_t(p) * size_t(q 
 
 namespace {
 
-// FP32-seeded rotations (rotation_fast) in the block kernel, opt-in (XRS_SVD_FAST_ROT=1). Measured
-// (profiles/r03/svd_rotation_ab_r03k.txt): 9 % fewer cycles per cross round (1409 vs 1547; the rotation
-// parameters are not the round's bottleneck), but the inexact angles cost a sweep at 128 x 128 flat
-// (11 vs 10): no net gain, so the fully Newton-refined FP64 angle stays the default.
-bool jacobi_fast_rotations() {
-    static const bool on = [] {
-        const char* e = std::getenv("XRS_SVD_FAST_ROT");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-
 // block kernel launch: nb = ceil(p / BR) rounded up to even, nb / 2 one-CU workgroups (<= 32 here:
 // co-resident on any MI355X, which the grid barrier needs)
 template <int BR, int G, int E, bool ACC>
@@ -648,7 +608,7 @@ void launch_blocks(xrs_handle_t h, const double* W, int ldw, bool trans, int p, 
     DevBuf slots(h, size_t(nb) * BR * E * G * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
     XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
     hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, G, E, ACC>), dim3(nb / 2), dim3(BR * G), 0, h->stream, W, ldw, int(trans), p, q, nb, sweeps,
-                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev, (stamps ? 1 : 0) | (jacobi_fast_rotations() ? 2 : 0));
+                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev, stamps ? 1 : 0);
     check_launch("k_jacobi_vt_blocks");
 }
 
@@ -660,12 +620,9 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
                 "jacobi_vt: need 1 <= p <= q, p <= 512 (one workgroup) or q <= 1024 (blocks)");
     XRS_REQUIRE(kernel >= 0 && kernel <= 2, "jacobi_vt: kernel is 0 (auto), 1 (one workgroup) or 2 (blocks)");
     KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * q * 6.0, 16.0 * double(p) * q);
-    // smallest p handed to the multi-workgroup block kernel (XRS_SVD_BLOCK_MIN tunes it; measured faster
-    // than the one-workgroup kernel from p = 64 on: 0.59 vs 0.73 ms at 64, 1.19 vs 2.62 ms at 128)
-    static const int block_min = [] {
-        const char* e = std::getenv("XRS_SVD_BLOCK_MIN");
-        return e ? std::atoi(e) : 32;
-    }();
+    // smallest p handed to the multi-workgroup block kernel (measured faster than the one-workgroup kernel
+    // from p = 64 on: 0.59 vs 0.73 ms at 64, 1.19 vs 2.62 ms at 128)
+    constexpr int block_min = 32;
     const bool blocks_ok = q <= 2 * SVB_QMAX;
     XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 1024");
     if (q > SVB_QMAX) {   // rows of up to 1024 columns: blocks of 8 rows (2 x 8 x 1024 doubles of LDS)
@@ -699,6 +656,24 @@ void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int
     else if (width <= 256) launch_blocks<16, 32, 8, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
     else if (width <= 512) launch_blocks<16, 32, 16, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
     else launch_blocks<8, 32, 32, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
+}
+
+int jacobi_settle(xrs_handle_t h, int* status_dev, int p, int q, const std::function<void(int kernel)>& rerun) {
+    int sweeps = 0;
+    read_status(h, status_dev, 1, &sweeps);
+    for (int attempt = 0; sweeps == -2 && attempt < 2; ++attempt) {
+        // one workgroup where it fits (no grid barrier at all), else the block kernel once more
+        const int kernel = (p <= SV_MAXP && attempt == 0) ? 1 : 2;
+        std::fprintf(stderr, "[xerus_amd warning] multi-workgroup Jacobi barrier timed out (%d x %d); rerun (kernel %d)\n", p, q, kernel);
+        XRS_HIP(hipMemsetAsync(status_dev, 0, 4, h->stream));
+        rerun(kernel);
+        read_status(h, status_dev, 1, &sweeps);
+    }
+    if (sweeps == -2) throw Error{XRS_ENUMERIC, "one-sided Jacobi: the multi-workgroup kernel's grid barrier timed out twice"};
+    if (sweeps < 0)
+        std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %d x %d matrix did not converge (status %d)\n", p, q,
+                     sweeps);
+    return sweeps;
 }
 
 // Right singular vectors of a g x g triangular factor F (rows of Vt, S descending) for the truncation

@@ -160,13 +160,15 @@ void truncate_edge(TT& t, size_t k, size_t max_rank, double eps, double soft) {
     DevBuf S(h, g * 8), Vt(h, g * g * 8), st(h, 64);
     XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
     jacobi_right_vectors(h, F, int(g), wide, S.d(), Vt.d(), st.as<int>(), 60);
+    // -2 (a grid-barrier poll of the block kernel timed out) leaves S / Vt invalid: recomputed on the rows of
+    // F; other negative statuses are non-convergence warnings, as the reference's dgesdd failure
+    // (blasLapackWrapper.cpp:216-224)
+    jacobi_settle(h, st.as<int>(), int(g), int(g), [&](int kernel) {
+        jacobi_vt(h, F, int(g), false, int(g), int(g), S.d(), Vt.d(), int(g), st.as<int>(), 60, kernel);
+    });
     std::vector<double> s(g);
     XRS_HIP(hipMemcpyAsync(s.data(), S.d(), g * 8, hipMemcpyDeviceToHost, h->stream));
-    int sweeps = 0;
-    read_status(h, st.as<int>(), 1, &sweeps);   // (synchronises, s is on the host too)
-    if (sweeps < 0)   // non-convergence is a warning, as the reference's dgesdd failure (blasLapackWrapper.cpp:216-224)
-        std::fprintf(stderr, "[xerus_amd warning] SVD failed: one-sided Jacobi of a %zu x %zu matrix did not converge (status %d)\n", g, g,
-                     sweeps);
+    host_wait(h);
     const size_t kk = svd_cut(s, max_rank, eps);
     double* T = t.alloc(m * kk);
     if (wide) gemm(h, T, m, kk, 1.0, F, g, false, g, Vt.d(), g, true);          // L V_kk = (U S)_kk
@@ -235,44 +237,10 @@ void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool d
     if (do_reduce) t.reduce(H[k], a * a);
 }
 
-// Step s of both chains as paired launches (gemm_pair): the two T products in one grid, then the two
-// Grams in one grid; with dry = true only reports whether both pairs would be taken. Boundary cores
-// (k = 0 left, k = d-1 right) have their own single products.
-bool paired_gram_step(TT& t, std::vector<double*>& G, std::vector<double*>& H, double* TL, double* TR, size_t kl, size_t kr,
-                      bool dry) {
-    const size_t last = t.d - 1;
-    if (kl == 0 || kr == last) {
-        if (dry) return false;
-        left_gram_step(t, G, TL, kl);
-        right_gram_step(t, H, TR, kr);
-        return false;
-    }
-    const size_t a = t.r[kl], b = t.r[kl + 1], cl = t.cols_right(kl);
-    const size_t a2 = t.r[kr], b2 = t.r[kr + 1], cr = t.cols_right(kr);
-    const GemmSpec l1{G[kl], t.core[kl], TL, a, cl, a, a, cl, false, false};               // G_k M_k
-    const GemmSpec r1{t.core[kr], H[kr + 1], TR, a2 * t.n[kr], b2, b2, b2, b2, false, false};  // M_k H_{k+1}
-    const GemmSpec l2{t.core[kl], TL, G[kl + 1], b, b, a * t.n[kl], b, b, true, false};      // M^T (G M)
-    const GemmSpec r2{t.core[kr], TR, H[kr], a2, a2, cr, cr, cr, false, true};               // M (M H)^T
-    if (dry) return gemm_pair(t.h, l1, r1, false, true) && gemm_pair(t.h, l2, r2, true, true);
-    bool paired = true;
-    if (!gemm_pair(t.h, l1, r1)) {
-        gemm(t.h, l1);
-        gemm(t.h, r1);
-        paired = false;
-    }
-    if (!gemm_pair(t.h, l2, r2, true)) {
-        gemm_sym(t.h, l2.C, l2.N, 1.0, l2.A, l2.lda, l2.ta, l2.K, l2.B, l2.ldb, l2.tb);
-        gemm_sym(t.h, r2.C, r2.N, 1.0, r2.A, r2.lda, r2.ta, r2.K, r2.B, r2.ldb, r2.tb);
-        paired = false;
-    }
-    return paired;
-}
-
 // Both chains (G: left Grams, only with `left`; H: right Grams; `store` owns the memory). Unsharded,
-// when every step pairs (paired_gram_step), they run on ONE stream as paired launches -- each grid holds
-// both chains' products, so a launch fills the chip instead of two kernels sharing it from two streams;
-// otherwise concurrently (left on a side stream, right on the main stream) with their launches
-// interleaved step by step. Sharded, step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s}
+// concurrently (left on a side stream, right on the main stream) with their launches interleaved step by
+// step. (Both chains' products as one two-entry grid on one stream measured slower: one chain's split-K
+// reduce and boundary products no longer overlap the other chain's GEMMs) Sharded, step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s}
 // sit side by side in one buffer.
 void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left) {
     const size_t d = t.d;
@@ -308,14 +276,6 @@ void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::v
         for (size_t k = d - 1; k >= 1; --k) right_gram_step(t, H, TR.d(), k);
         return;
     }
-    // one stream with paired launches when most steps pair (the unpaired ones -- boundary cores, odd
-    // ranks -- then run their two chains back to back), else two streams
-    size_t npair = 0;
-    for (size_t s = 0; s + 1 < d; ++s) npair += paired_gram_step(t, G, H, TL.d(), TR.d(), s, d - 1 - s, true) ? 1 : 0;
-    if (2 * npair >= d - 1 && npair >= 2) {
-        for (size_t s = 0; s + 1 < d; ++s) paired_gram_step(t, G, H, TL.d(), TR.d(), s, d - 1 - s, false);
-        return;
-    }
     StreamFork fork(h);
     for (size_t s = 0; s + 1 < d; ++s) {
         fork.side();
@@ -326,9 +286,9 @@ void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::v
     fork.join();
 }
 
-// Host-side phase timestamps of round() (XRS_ROUND_TIMING=1: one stderr line per round; diagnostics only)
+// Host-side phase timestamps of round() (XRS_STAMPS=round: one stderr line per round; diagnostics only)
 struct HostMarks {
-    bool on = std::getenv("XRS_ROUND_TIMING") != nullptr;
+    bool on = stamps_enabled("round");
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
     std::string line;
     void mark(const char* what) {
@@ -722,17 +682,16 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     }
     // L_k and Z_k of the register-resident kernels (r <= 256) hold exact zeros above the diagonal: their
     // zero K-blocks are skipped (5/8 of the work at r = 256)
-    static const bool no_tri = std::getenv("XRS_NO_TRI") != nullptr;
     std::vector<GemmJob> right, left;
     for (size_t k = 0; k + 1 < d; ++k) {   // right factors: M_k (I (x) L_{k+1}), (r_k n_k) x r_{k+1} x r_{k+1}
         const size_t b = t.r[k + 1];
         right.push_back({t.rows_left(k), b, b, b, b, false, false, t.core[k], Lf[k + 1].d(), k == 0 ? out.C[k] : W[k].d()});
-        right.back().tri = (b <= 256 && !no_tri) ? kTriB : 0;
+        right.back().tri = b <= 256 ? kTriB : 0;
     }
     for (size_t k = 1; k < d; ++k) {       // left factors: Z_k (r_k x r_k) times the r_k x (n_k r_{k+1}) unfolding
         const size_t a = t.r[k], cols = t.cols_right(k);
         left.push_back({a, cols, a, a, cols, false, false, Z[k].d(), k + 1 < d ? W[k].d() : t.core[k], out.C[k]});
-        left.back().tri = (a <= 256 && !no_tri) ? kTriA : 0;
+        left.back().tri = (a <= 256 && true) ? kTriA : 0;
     }
     gemm_grouped(h, right);
     gemm_grouped(h, left);
@@ -970,24 +929,7 @@ double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx
             R.g2 = GemmSpec{T, Y[k], nb + (shard ? ne : emax), a, b, nk * b2, nk * b2, nk * b2, false, true};   // T Y_k^T
         }
     };
-    // both ends on ONE stream as paired launches (gemm_pair) when most steps pair; else the left end on a
-    // side stream beside the right end on the main stream (and always so when sharded)
-    size_t npair = 0;
-    if (!shard) {
-        double *E = P0.d(), *F = P0.d() + emax, *nb = P1.d(), *cb = P0.d();
-        for (size_t s = 0; s < steps; ++s) {
-            EndStep L, R;
-            size_t ne;
-            plan(s, E, F, nb, L, R, ne);
-            if (L.on && R.on && L.first && R.first && gemm_pair(h, L.g1, R.g1, false, true) &&
-                gemm_pair(h, L.g2, R.g2, false, true))
-                ++npair;
-            if (L.on) E = L.g2.C;
-            if (R.on) F = R.g2.C;
-            std::swap(cb, nb);
-        }
-    }
-    const bool paired = !shard && 2 * npair >= steps && npair >= 2;
+    // the left end on a side stream beside the right end on the main stream (one stream when sharded)
     double *E = P0.d(), *F = P0.d() + emax;
     double* nextbuf = P1.d();
     double* curbuf = P0.d();
@@ -997,26 +939,15 @@ double dot_two_ended(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx
             EndStep L, R;
             size_t ne;
             plan(s, E, F, nextbuf, L, R, ne);
-            if (paired && L.on && R.on && L.first == R.first) {
-                if (L.first && !gemm_pair(h, L.g1, R.g1)) {
-                    gemm(h, L.g1);
-                    gemm(h, R.g1);
-                }
-                if (!gemm_pair(h, L.g2, R.g2)) {
-                    gemm(h, L.g2);
-                    gemm(h, R.g2);
-                }
-            } else {
-                if (L.on) {
-                    if (!shard && !paired) fork.side();
-                    if (L.first) gemm(h, L.g1);
-                    gemm(h, L.g2);
-                }
-                if (R.on) {
-                    if (!shard && !paired) fork.main();
-                    if (R.first) gemm(h, R.g1);
-                    gemm(h, R.g2);
-                }
+            if (L.on) {
+                if (!shard) fork.side();
+                if (L.first) gemm(h, L.g1);
+                gemm(h, L.g2);
+            }
+            if (R.on) {
+                if (!shard) fork.main();
+                if (R.first) gemm(h, R.g1);
+                gemm(h, R.g2);
             }
             // one all-reduce for both ends. The left end is idle only in the last step of an odd order
             // (d - m = m + 1): E then stays in the other buffer, untouched by this step's F.

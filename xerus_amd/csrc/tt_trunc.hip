@@ -322,8 +322,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     std::vector<int*> jst;   // Jacobi statuses
     // certificates of the eigensolver edges on side stream 0 (off the sweep's critical path), when this
     // handle owns its streams and is not inside a fork
-    static const bool cert_side_env = std::getenv("XRS_TRUNC_CERT_INLINE") == nullptr;
-    const bool cert_side = cert_side_env && !h->borrowed_streams && h->stream == h->own_stream && h->side_stream[0];
+    const bool cert_side = !h->borrowed_streams && h->stream == h->own_stream && h->side_stream[0] && h->prof_mask == 0;
     bool side_used = false;
     for (size_t k = d - 1; k >= 1; --k) {
         const size_t r = rr[k], N = t.n[k] * rr[k + 1], Ng = ng[k] * rr[k + 1];   // local / global columns
@@ -366,11 +365,9 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
             pb.status = status + nst;
             XRS_HIP(hipEventRecord(h->ev_fork, h->stream));
             XRS_HIP(hipStreamWaitEvent(h->side_stream[0], h->ev_fork, 0));
-            hipStream_t main_stream = h->stream;
-            h->stream = h->side_stream[0];
-            potrf_batched(h, pb, 1);
-            h->stream = main_stream;
             side_used = true;
+            StreamSwap on_side(h, h->side_stream[0]);   // (restores h->stream on scope exit, also on a throw)
+            potrf_batched(h, pb, 1);
             nst += 1;
         } else {
             std::vector<CholJob> cj{{P, int(g), nullptr, nullptr}};
