@@ -54,6 +54,8 @@ SIGNATURES = {
     "xrs_solve_least_squares": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ, _DP, _SZ]),
     "xrs_svd_rows_vt": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ, C.c_int]),
     "xrs_sym_eig_top": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ]),
+    "xrs_tt_entrywise_product": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ), C.POINTER(_DP),
+                                           C.c_double, C.POINTER(_DP)]),
     "xrs_tt_operator_apply": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                         C.POINTER(_SZ), C.POINTER(_DP), C.c_int, C.POINTER(_DP)]),
     "xrs_tt_move_core": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.c_int, _SZ, _SZ, C.c_int]),

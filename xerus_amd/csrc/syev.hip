@@ -449,24 +449,40 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 // one 64-lane workgroup per wanted eigenvalue: block q -> the q-th largest (ascending index n - 1 - q).
 // Zt (kk x ldz): row q = the eigenvector of T (normalised); lam[q]. status[0] <- -1 if a multisection
 // did not reach full precision.
+//
+// Every O(n) recurrence here is a dependent chain, so the kernel is written for chain latency:
+//  * Sturm counts (multisection, lane l at the point lo + (hi - lo)(l + 1)/65) by the three-term recurrence
+//    p_k = (d_k - x) p_{k-1} - e_{k-1}^2 p_{k-2} (one FMA per level on the chain, instead of a reciprocal
+//    and its Newton steps in the ratio form q_k = p_k / p_{k-1}); #{lambda < x} = sign changes of p_0..p_n
+//    (Barth, Martin & Wilkinson), an exact zero p_k taken as q_k = -pivmin (dlaebz's rule), the pair
+//    (p_{k-1}, p_k) rescaled by a power of two every 8 levels (no over/underflow, signs unchanged). The
+//    operands are uniform across lanes: blocks of 8 are read from LDS one block ahead of the chain.
+//  * inverse iteration: the partially pivoted LU of T - lambda I (dgttrf) as a streaming recurrence whose
+//    running pivot row stays in registers (factors stored to LDS, off the chain), the solves (dgttrs) with
+//    their operands prefetched a block ahead. (The first version kept every running value in LDS: each
+//    level waited on LDS round trips, ~100 us per eigenvalue set at n = 128.)
 template <int NEWTON>
 __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
                                                      double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status) {
-    __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX];
-    __shared__ double ld[SY_MAX], ldl[SY_MAX], ldu[SY_MAX], ldu2[SY_MAX], lb[SY_MAX];
-    __shared__ int lpiv[SY_MAX];
+    constexpr int B8 = 8;
+    __shared__ double sd[SY_MAX + 2 * B8], se[SY_MAX + 2 * B8], se2[SY_MAX + 2 * B8];
+    __shared__ double ud[SY_MAX], uu[SY_MAX], uu2[SY_MAX], ul[SY_MAX], lb[SY_MAX];
+    __shared__ int upv[SY_MAX];
     const int lane = threadIdx.x, q = blockIdx.x, m = n - 1 - q;
     double gl = 1e300, gu = -1e300, emax2 = 0.0, amax = 0.0;
-    for (int i = lane; i < n; i += 64) {
-        const double di = d[i], ei = i + 1 < n ? e[i] : 0.0, em = i > 0 ? e[i - 1] : 0.0;
+    for (int i = lane; i < n + 2 * B8; i += 64) {
+        const bool in = i < n;
+        const double di = in ? d[i] : 0.0, ei = i + 1 < n ? e[i] : 0.0, em = (in && i > 0) ? e[i - 1] : 0.0;
         sd[i] = di;
         se[i] = ei;
         se2[i] = ei * ei;
-        const double r = fabs(ei) + fabs(em);
-        gl = fmin(gl, di - r);
-        gu = fmax(gu, di + r);
-        emax2 = fmax(emax2, ei * ei);
-        amax = fmax(amax, fabs(di) + r);
+        if (in) {
+            const double r = fabs(ei) + fabs(em);
+            gl = fmin(gl, di - r);
+            gu = fmax(gu, di + r);
+            emax2 = fmax(emax2, ei * ei);
+            amax = fmax(amax, fabs(di) + r);
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -475,6 +491,20 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         emax2 = fmax(emax2, __shfl_xor(emax2, o, 64));
         amax = fmax(amax, __shfl_xor(amax, o, 64));
     }
+    // T scaled by a power of two to ||T|| ~ 1 (the recurrences then neither overflow nor underflow within
+    // their 8-level rescaling blocks); the eigenvalue is scaled back, the eigenvector is unaffected
+    const int tex = amax > 0.0 ? __builtin_amdgcn_frexp_exp(amax) : 0;
+    const double tsc = __builtin_amdgcn_ldexp(1.0, -tex);
+    __syncthreads();
+    for (int i = lane; i < n; i += 64) {
+        sd[i] *= tsc;
+        se[i] *= tsc;
+        se2[i] *= tsc * tsc;
+    }
+    gl *= tsc;
+    gu *= tsc;
+    emax2 *= tsc * tsc;
+    amax *= tsc;
     __syncthreads();
     const double pivmin = 1e-290 * fmax(1.0, emax2);
     const double span = fmax(gu - gl, 1e-300);
@@ -484,13 +514,38 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     bool done = false;
     for (; rounds < 16 && !done; ++rounds) {
         const double x = lo + (hi - lo) * double(lane + 1) * (1.0 / 65.0);
-        double qv = sd[0] - x;
-        if (fabs(qv) < pivmin) qv = -pivmin;
-        int c = qv < 0.0;
-        for (int i = 1; i < n; ++i) {
-            qv = (sd[i] - x) - se2[i - 1] * rcpn<NEWTON>(qv);
-            if (fabs(qv) < pivmin) qv = -pivmin;
-            c += qv < 0.0;
+        double pm = 1.0, p = sd[0] - x;   // p_0 = 1, p_1 = d_0 - x
+        if (p == 0.0) p = -pivmin;
+        int c = p < 0.0;
+        double dn[B8], en[B8];
+#pragma unroll
+        for (int u = 0; u < B8; ++u) {
+            dn[u] = sd[1 + u];
+            en[u] = se2[u];
+        }
+        for (int i0 = 1; i0 < n; i0 += B8) {
+            double dc[B8], ec[B8];
+#pragma unroll
+            for (int u = 0; u < B8; ++u) {
+                dc[u] = dn[u];
+                ec[u] = en[u];
+                dn[u] = sd[i0 + B8 + u];   // next block (padded: reads stay inside the arrays)
+                en[u] = se2[i0 + B8 - 1 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < B8; ++u) {
+                if (i0 + u < n) {
+                    double pn = fma(dc[u] - x, p, -ec[u] * pm);
+                    if (pn == 0.0) pn = -pivmin * p;
+                    c += (pn < 0.0) != (p < 0.0);
+                    pm = p;
+                    p = pn;
+                }
+            }
+            // rescale the pair by a power of two (signs and ratios unchanged)
+            const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(p), fabs(pm)));
+            p = __builtin_amdgcn_ldexp(p, -ex);
+            pm = __builtin_amdgcn_ldexp(pm, -ex);
         }
         double nlo = c <= m ? x : -1e300, nhi = c >= m + 1 ? x : 1e300;
 #pragma unroll
@@ -504,72 +559,120 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         done = (hi - lo) <= 2.2204460492503131e-16 * (2.0 * fmax(fabs(lo), fabs(hi)) + 4.0 * span) + 2.0 * pivmin;
     }
     const double lmb = 0.5 * (lo + hi);
-    __shared__ double ild[SY_MAX];   // inverse pivots of U
+    const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
     if (lane == 0) {
-        lam[q] = lmb;
+        lam[q] = __builtin_amdgcn_ldexp(lmb, tex);
         if (!done) atomicMin(status, -1);
-        // inverse iteration: T - lambda I = P L U (dgttrf, row interchanges where the subdiagonal entry is
-        // larger), tiny pivots replaced by u ||T|| (dlagtf's perturbation)
-        for (int i = 0; i < n; ++i) {
-            ld[i] = sd[i] - lmb;
-            ldl[i] = i + 1 < n ? se[i] : 0.0;
-            ldu[i] = i + 1 < n ? se[i] : 0.0;
-            ldu2[i] = 0.0;
-            lpiv[i] = i;
+        // LU of T - lambda I with row interchanges where the subdiagonal entry is larger (dgttrf); the
+        // running pivot row (a, b) = (diagonal, superdiagonal) of row i after the earlier eliminations.
+        // Outputs per row: U diagonal ud (tiny pivots replaced by u ||T||, dlagtf's perturbation, stored
+        // inverted), U super- / second superdiagonal uu, uu2, multiplier ul, interchange flag upv.
+        double a = sd[0] - lmb, b = se[0];
+        double sub[B8], dnx[B8], unx[B8];
+#pragma unroll
+        for (int u = 0; u < B8; ++u) {
+            sub[u] = se[u];
+            dnx[u] = sd[1 + u] - lmb;
+            unx[u] = se[1 + u];
         }
-        for (int i = 0; i + 1 < n; ++i) {
-            if (fabs(ld[i]) >= fabs(ldl[i])) {
-                if (ld[i] != 0.0) {
-                    const double f = ldl[i] * rcpn<NEWTON>(ld[i]);
-                    ldl[i] = f;
-                    ld[i + 1] -= f * ldu[i];
+        for (int i0 = 0; i0 + 1 < n; i0 += B8) {
+            double s_[B8], dx[B8], ux[B8];
+#pragma unroll
+            for (int u = 0; u < B8; ++u) {
+                s_[u] = sub[u];
+                dx[u] = dnx[u];
+                ux[u] = unx[u];
+                sub[u] = se[i0 + B8 + u];
+                dnx[u] = sd[i0 + B8 + 1 + u] - lmb;
+                unx[u] = se[i0 + B8 + 1 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < B8; ++u) {
+                const int i = i0 + u;
+                if (i + 1 < n) {
+                    if (fabs(a) >= fabs(s_[u])) {   // no interchange
+                        const double f = a != 0.0 ? s_[u] * rcpn<NEWTON>(a) : 0.0;
+                        ud[i] = a;
+                        uu[i] = b;
+                        uu2[i] = 0.0;
+                        ul[i] = f;
+                        upv[i] = 0;
+                        a = fma(-f, b, dx[u]);
+                        b = ux[u];
+                    } else {                        // rows i and i+1 interchanged
+                        const double f = a * rcpn<NEWTON>(s_[u]);
+                        ud[i] = s_[u];
+                        uu[i] = dx[u];
+                        uu2[i] = i + 2 < n ? ux[u] : 0.0;
+                        ul[i] = f;
+                        upv[i] = 1;
+                        a = fma(-f, dx[u], b);
+                        b = i + 2 < n ? -f * ux[u] : 0.0;
+                    }
                 }
-            } else {
-                const double f = ld[i] * rcpn<NEWTON>(ldl[i]);
-                ld[i] = ldl[i];
-                ldl[i] = f;
-                const double tmp = ldu[i];
-                ldu[i] = ld[i + 1];
-                ld[i + 1] = tmp - f * ld[i + 1];
-                if (i + 2 < n) {
-                    ldu2[i] = ldu[i + 1];
-                    ldu[i + 1] = -f * ldu[i + 1];
-                }
-                lpiv[i] = i + 1;
             }
         }
+        ud[n - 1] = a;
     }
     __syncthreads();
-    {
-        const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
-        for (int i = lane; i < n; i += 64) {
-            double p = ld[i];
-            if (fabs(p) < tiny) p = copysign(tiny, p == 0.0 ? 1.0 : p);
-            ild[i] = rcp2(p);
-            lb[i] = 1.0 + double((i * 37 + q * 11) % 17) * (1.0 / 17.0);
-        }
+    for (int i = lane; i < n; i += 64) {
+        double p = ud[i];
+        if (fabs(p) < tiny) p = copysign(tiny, p == 0.0 ? 1.0 : p);
+        ud[i] = rcp2(p);   // inverse pivots
+        lb[i] = 1.0 + double((i * 37 + q * 11) % 17) * (1.0 / 17.0);
     }
     __syncthreads();
     for (int it = 0; it < 3; ++it) {
-        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in registers)
+        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution, operands a block ahead
             double cur = lb[0];
-            for (int i = 0; i + 1 < n; ++i) {
-                const double nxt = lb[i + 1], f = ldl[i];
-                if (lpiv[i] == i) {
-                    lb[i] = cur;
-                    cur = fma(-f, cur, nxt);
-                } else {
-                    lb[i] = nxt;
-                    cur = fma(-f, nxt, cur);
+            for (int i0 = 0; i0 + 1 < n; i0 += B8) {
+                double f[B8], nx[B8];
+                int pv[B8];
+#pragma unroll
+                for (int u = 0; u < B8; ++u) {
+                    const int i = i0 + u;
+                    const bool in = i + 1 < n;
+                    f[u] = in ? ul[i] : 0.0;
+                    nx[u] = in ? lb[i + 1] : 0.0;
+                    pv[u] = in ? upv[i] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < B8; ++u) {
+                    const int i = i0 + u;
+                    if (i + 1 < n) {
+                        if (pv[u] == 0) {
+                            lb[i] = cur;
+                            cur = fma(-f[u], cur, nx[u]);
+                        } else {
+                            lb[i] = nx[u];
+                            cur = fma(-f[u], nx[u], cur);
+                        }
+                    }
                 }
             }
-            double x1 = cur * ild[n - 1], x2 = 0.0;
+            double x1 = cur * ud[n - 1], x2 = 0.0;
             lb[n - 1] = x1;
-            for (int i = n - 2; i >= 0; --i) {
-                const double x0 = (lb[i] - ldu[i] * x1 - ldu2[i] * x2) * ild[i];
-                lb[i] = x0;
-                x2 = x1;
-                x1 = x0;
+            for (int i1 = n - 2; i1 >= 0; i1 -= B8) {
+                double rb[B8], u1[B8], u2[B8], iv[B8];
+#pragma unroll
+                for (int u = 0; u < B8; ++u) {
+                    const int i = i1 - u;
+                    const bool in = i >= 0;
+                    rb[u] = in ? lb[i] : 0.0;
+                    u1[u] = in ? uu[i] : 0.0;
+                    u2[u] = in ? uu2[i] : 0.0;
+                    iv[u] = in ? ud[i] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < B8; ++u) {
+                    const int i = i1 - u;
+                    if (i >= 0) {
+                        const double x0 = fma(-u1[u], x1, fma(-u2[u], x2, rb[u])) * iv[u];
+                        lb[i] = x0;
+                        x2 = x1;
+                        x1 = x0;
+                    }
+                }
             }
         }
         __syncthreads();
