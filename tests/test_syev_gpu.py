@@ -44,3 +44,25 @@ def test_sym_eig_top_lower_triangle_only(handle):
     lam, Ut, st = handle.sym_eig_top(handle.array(Al), 10)
     assert st == 0
     assert np.abs(lam.numpy() - np.linalg.eigvalsh(A)[::-1][:10]).max() <= 1e-13 * 5
+
+
+@pytest.mark.parametrize("n,kk", [(24, 12), (96, 40), (200, 120)])
+def test_sym_eig_top_clusters(handle, n, kk):
+    """Exactly repeated and 1e-9-close eigenvalues inside the kept set (inverse iteration alone gives
+    non-orthogonal vectors there; k_cluster_orth orthonormalises each cluster): eigenvalues, orthonormality
+    and residuals at the same bars, and the kept subspace equals LAPACK's when the cut lies in a gap."""
+    rng = np.random.default_rng(n)
+    spec = np.concatenate([np.repeat([9.0, 7.0, 5.0], 4), 5.0 - 1e-9 * np.arange(1, 4), 1.0 + rng.random(n - 15)])
+    A = _spd(n, spec, n + 3)
+    A = 0.5 * (A + A.T)
+    lam, Ut, st = handle.sym_eig_top(handle.array(A), kk)
+    assert st == 0
+    lam, U = lam.numpy(), Ut.numpy().T
+    w, Z = np.linalg.eigh(A)
+    nrm = np.linalg.norm(A, 2)
+    assert np.abs(lam - w[::-1][:kk]).max() <= 1e-13 * nrm
+    assert np.abs(U.T @ U - np.eye(kk)).max() <= 1e-12
+    assert np.linalg.norm(A @ U - U * lam, axis=0).max() <= 1e-12 * nrm
+    P = Z[:, ::-1][:, :kk]
+    if w[::-1][kk - 1] - w[::-1][kk] > 1e-3:   # the projector onto the kept subspace is unique
+        assert np.abs(U @ U.T - P @ P.T).max() <= 1e-11

@@ -54,6 +54,7 @@ SIGNATURES = {
     "xrs_solve_least_squares": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ, _DP, _SZ]),
     "xrs_svd_rows_vt": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ, C.c_int]),
     "xrs_sym_eig_top": (C.c_int, [_DP, _DP, _DP, C.POINTER(C.c_int), _DP, _SZ, _SZ]),
+    "xrs_sym_tridiag": (C.c_int, [_DP, _DP, _DP, _DP, _SZ]),
     "xrs_tt_entrywise_product": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ), C.POINTER(_DP),
                                            C.c_double, C.POINTER(_DP)]),
     "xrs_tt_operator_apply": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
@@ -294,6 +295,13 @@ class Handle:
         lam, Ut, st = self.empty((kk,)), self.empty((kk, n)), C.c_int()
         _check("xrs_sym_eig_top", self.lib.xrs_sym_eig_top(self.h, _DP(lam.ptr), _DP(Ut.ptr), C.byref(st), _DP(A.ptr), n, kk))
         return lam, Ut, st.value
+
+    def sym_tridiag(self, A: "DeviceArray"):
+        """(d, e) of the two-stage tridiagonalisation of the symmetric A (xrs_sym_tridiag)."""
+        n = A.shape[0]
+        d, e = self.empty((n,)), self.empty((n,))
+        _check("xrs_sym_tridiag", self.lib.xrs_sym_tridiag(self.h, _DP(d.ptr), _DP(e.ptr), _DP(A.ptr), n))
+        return d.numpy(), e.numpy()[: n - 1]
 
     def svd_rows_vt(self, A: "DeviceArray", kernel: int = 0):
         """(S, Vt, sweeps) of the rows of A (p <= q <= 512) by one-sided Jacobi (xrs_svd_rows_vt)."""

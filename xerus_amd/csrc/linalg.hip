@@ -40,37 +40,6 @@ int read_status(xrs_handle_t h, const int* status_dev, int count, int* host_out)
     return any;
 }
 
-// first index of the max-norm column (rows=false) or row (rows=true) and the entry A[0][p] / A[p][0]
-__global__ void __launch_bounds__(1024) k_argmax_norm(const double* __restrict__ A, int m, int n, int rows,
-                                                      double* __restrict__ out) {
-    __shared__ double sv[16];
-    __shared__ int si[16];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int cnt = rows ? m : n, len = rows ? n : m;
-    double best = -1.0;
-    int bi = cnt;
-    for (int j = wave; j < cnt; j += 16) {
-        double s = 0.0;
-        for (int i = lane; i < len; i += 64) {
-            const double v = rows ? A[size_t(j) * n + i] : A[size_t(i) * n + j];
-            s += v * v;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-        if (s > best) { best = s; bi = j; }
-    }
-    if (lane == 0) { sv[wave] = best; si[wave] = bi; }
-    __syncthreads();
-    if (tid == 0) {
-        double bv = -1.0;
-        int b = cnt;
-        for (int w = 0; w < 16; ++w)
-            if (sv[w] > bv || (sv[w] == bv && si[w] < b)) { bv = sv[w]; b = si[w]; }
-        out[0] = double(b);
-        out[1] = rows ? A[size_t(b) * n] : A[b];
-    }
-}
-
 __global__ void __launch_bounds__(256) k_dev_identity(const double* __restrict__ G, int n, double* __restrict__ out) {
     __shared__ double red[4];
     double mx = 0.0;
@@ -130,21 +99,6 @@ static double max_abs_dev_identity(xrs_handle_t h, const double* G, size_t n) {
     XRS_HIP(hipStreamSynchronize(h->stream));
     const double v = hs[0];
     return (v == v) ? v : 1e300;
-}
-
-// dgeqp3's R_00 > 0 iff the first entry of the pivot column is negative (dlarfg: beta = -sign(alpha)*norm);
-// for a single-row problem (dlarfg with N = 1) R_00 = alpha itself.
-static bool reference_r00_positive(xrs_handle_t h, const double* A, size_t m, size_t n, bool rows) {
-    double* out = static_cast<double*>(h->dev_scratch) + 16;
-    hipLaunchKernelGGL(k_argmax_norm, dim3(1), dim3(1024), 0, h->stream, A, int(m), int(n), int(rows), out);
-    check_launch("k_argmax_norm");
-    double* hs = static_cast<double*>(h->host_scratch) + 16;
-    XRS_HIP(hipMemcpyAsync(hs, out, 16, hipMemcpyDeviceToHost, h->stream));
-    XRS_HIP(hipStreamSynchronize(h->stream));
-    const double alpha = hs[1];
-    const size_t len = rows ? n : m;
-    if (len <= 1) return alpha > 0.0;
-    return alpha < 0.0 || (alpha == 0.0 && std::signbit(alpha));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -342,15 +296,10 @@ size_t qc(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double
     }
     // certified: sigma_min >= cert*||A||_F > 16 u R_00 (R_00 <= ||A||_F) -> rank n
     if (o.certified && o.cert_ratio > 64.0 * kDblEps) return n;
-    if (!reference_r00_positive(h, A, m, n, false)) return n;  // reference never reduces rank then
-    // exact pivoted rank on the triangular factor (same column norms as A up to rounding)
-    DevBuf Rc(h, n * n * 8), Q2(h, n * n * 8), Cq(h, n * n * 8), Qo(h, m * n * 8);
-    XRS_HIP(hipMemcpyAsync(Rc.d(), C, n * n * 8, hipMemcpyDeviceToDevice, h->stream));
-    const size_t r = qrcp(h, Rc.d(), n, n, Q2.d(), Cq.d(), true, true, true);
-    XRS_HIP(hipMemcpyAsync(Qo.d(), Q, m * n * 8, hipMemcpyDeviceToDevice, h->stream));
-    gemm(h, Q, m, r, 1.0, Qo.d(), n, false, n, Q2.d(), n, false);   // Q = Q * Q2[:, :r]  (ldb = n, first r cols)
-    XRS_HIP(hipMemcpyAsync(C, Cq.d(), r * n * 8, hipMemcpyDeviceToDevice, h->stream));
-    return r;
+    // not certified: (numerically) rank-deficient or nearly so. A Gram-based factor of such an A is accurate only
+    // to ~kappa u in its near-null directions (an entrywise-product TT moved to core 0 measured 5e-12 relative
+    // error through the former pivoted QR of the CholeskyQR factor), so the dgeqp3 emulation runs on A itself
+    return exact();
 }
 
 // CQ: the reference runs col-major dgeqp3 on A^T (blasLapackWrapper.cpp:317-371), i.e. QC of A^T.
@@ -376,14 +325,7 @@ size_t cq(xrs_handle_t h, const double* A, size_t m, size_t n, double* C, double
         return exact();
     }
     if (o.certified && o.cert_ratio > 64.0 * kDblEps) return m;
-    if (!reference_r00_positive(h, A, m, n, true)) return m;
-    DevBuf Lt(h, m * m * 8), Q2(h, m * m * 8), C2(h, m * m * 8), Qo(h, m * n * 8);
-    transpose(h, Lt.d(), C, m, m);                                // A^T = Q^T L^T
-    const size_t r = qrcp(h, Lt.d(), m, m, Q2.d(), C2.d(), true, true, true);   // L^T P = Q2 R2
-    XRS_HIP(hipMemcpyAsync(Qo.d(), Q, m * n * 8, hipMemcpyDeviceToDevice, h->stream));
-    gemm(h, Q, r, n, 1.0, Q2.d(), m, true, m, Qo.d(), n, false);   // Q = Q2[:, :r]^T Q
-    transpose(h, C, C2.d(), r, m);                                // C = C2^T (m x r)
-    return r;
+    return exact();   // (see qc)
 }
 
 void qr(xrs_handle_t h, const double* A, size_t m, size_t n, double* Q, double* R) {
@@ -533,6 +475,16 @@ int xrs_sym_eig_top(xrs_handle_t h, double* lam, double* Ut, int* status, const 
         XRS_HIP(hipMemsetAsync(st.d(), 0, 64, h->stream));
         sym_eig_top(h, A, int(n), int(n), int(kk), lam, nullptr, Ut, int(n), st.as<int>());
         read_status(h, st.as<int>(), 1, status);
+    });
+}
+
+int xrs_sym_tridiag(xrs_handle_t h, double* d, double* e, const double* A, size_t n) {
+    return guarded([&] {
+        XRS_REQUIRE(h && d && e && A, "null argument");
+        XRS_REQUIRE(n >= 2 && n <= 256, "xrs_sym_tridiag: need 2 <= n <= 256");
+        fence_readers(h);
+        sym_tridiag_2stage(h, A, int(n), int(n), d, e, nullptr, nullptr, nullptr);
+        XRS_HIP(hipStreamSynchronize(h->stream));
     });
 }
 
