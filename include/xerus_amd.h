@@ -142,9 +142,8 @@ int xrs_solve_least_squares(xrs_handle_t handle, double* X, const double* A, siz
  *  kernel: 0 auto, 1 one workgroup, 2 multi-workgroup blocks (p > 16). *sweeps (host): Jacobi
  *  sweeps used, -1 not converged, -2 grid-barrier timeout. Synchronises. */
 int xrs_svd_rows_vt(xrs_handle_t handle, double* S, double* Vt, int* sweeps, const double* A, size_t p, size_t q, int kernel);
-/** Two-stage tridiagonalisation of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 256): dense ->
- *  band of width 16 (blocked Householder panels, MFMA trailing updates), band -> tridiagonal (bulge chasing);
- *  d (n) and e (n - 1) of T = Q^T A Q. The first stage of the truncating round's eigensolver (dsytrd's role,
+/** Householder tridiagonalisation of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 256) in one
+ *  register-resident workgroup; d (n) and e (n - 1) of T = Q^T A Q. The first stage of the truncating round's eigensolver (dsytrd's role,
  *  tensor.cpp:1424-1489 via the certified edge Gram); exposed for its tests. Synchronises. */
 int xrs_sym_tridiag(xrs_handle_t handle, double* d, double* e, const double* A, size_t n);
 /** Eigenpairs of the kk largest eigenvalues of a symmetric n x n matrix A (lower triangle read, 2 <= n <= 256,

@@ -1,4 +1,4 @@
-"""The two-stage tridiagonalisation (xrs_sym_tridiag: dense -> band of width 16 -> tridiagonal, csrc/syev.hip)
+"""The Householder tridiagonalisation (xrs_sym_tridiag: k_sytrd / k_sytrd_l512, csrc/syev.hip)
 against LAPACK (numpy / scipy): T = Q^T A Q has A's eigenvalues. Bar: eigenvalues of T equal eigvalsh(A) to
 1e-13 ||A|| (backward stable: u ||A|| times a small multiple). Orders around the band and panel edges."""
 import numpy as np

@@ -297,7 +297,7 @@ class Handle:
         return lam, Ut, st.value
 
     def sym_tridiag(self, A: "DeviceArray"):
-        """(d, e) of the two-stage tridiagonalisation of the symmetric A (xrs_sym_tridiag)."""
+        """(d, e) of the Householder tridiagonalisation of the symmetric A (xrs_sym_tridiag)."""
         n = A.shape[0]
         d, e = self.empty((n,)), self.empty((n,))
         _check("xrs_sym_tridiag", self.lib.xrs_sym_tridiag(self.h, _DP(d.ptr), _DP(e.ptr), _DP(A.ptr), n))

@@ -483,7 +483,7 @@ int xrs_sym_tridiag(xrs_handle_t h, double* d, double* e, const double* A, size_
         XRS_REQUIRE(h && d && e && A, "null argument");
         XRS_REQUIRE(n >= 2 && n <= 256, "xrs_sym_tridiag: need 2 <= n <= 256");
         fence_readers(h);
-        sym_tridiag_2stage(h, A, int(n), int(n), d, e, nullptr, nullptr, nullptr);
+        sym_tridiag(h, A, int(n), int(n), d, e);
         XRS_HIP(hipStreamSynchronize(h->stream));
     });
 }

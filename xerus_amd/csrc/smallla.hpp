@@ -72,8 +72,8 @@ bool jacobi_vt_fits_lds(int p, int q);
 // multisection did not converge (left untouched otherwise). Enqueued only.
 bool sym_eig_top_fits(int n, int kk);   // the truncating round's policy (n <= 256 unless XRS_SYEV_MAX lowers it)
 void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status_dev);
-// two-stage tridiagonalisation (syev.hip): d (n), e (n - 1) of T = Q^T A Q; V, Tp, refl optional (reflectors)
-void sym_tridiag_2stage(xrs_handle_t h, const double* A, int lda, int n, double* d, double* e, double* V, double* Tp, double* refl);
+// Householder tridiagonalisation (syev.hip's k_sytrd): d (n), e (n - 1) of T = Q^T A Q
+void sym_tridiag(xrs_handle_t h, const double* A, int lda, int n, double* d, double* e);
 bool jacobi_usv_fits(int p, int q);
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
                 int* status_dev, int max_sweeps = 40);

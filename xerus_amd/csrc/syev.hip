@@ -17,9 +17,12 @@
 //      rounds, same 105 us: every O(n) chain is bound by its ~20-cycle dependent FP64 latency per level).
 //   3. k_ormtr: the eigenvectors back to A's coordinates, u = H_0 ... H_{n-2} z, one wave per vector
 //      (64 lanes, 4 vectors per workgroup), the reflectors staged through LDS in chunks.
-// Inverse iteration is accurate for eigenvalues separated relative to ||T|| (the certified rounds' random
-// spectra); a cluster would give non-orthogonal vectors, which the round's final orthonormality check
-// rejects (then the reference's algorithm runs).
+//   2b. k_cluster_orth: vectors of eigenvalue clusters (gaps <= 1e-3 ||T||, dstein's ORTOL) orthonormalised
+//      by two modified Gram-Schmidt passes (dstein's reorthogonalisation within a cluster).
+// Measured dead end (round 4, profiles/r04/twostage_*_r04h.*): a two-stage tridiagonalisation (dense -> band
+// 16 by MFMA panel updates, band -> tridiagonal by bulge chasing, Q2/Q1 back-transformation) ran 303 + 333
+// + 186 us at n = 128 against this kernel's 330 us (cfg3 round(64): 8.25 vs 4.5 ms): in one workgroup every
+// panel and bulge step is a chain of LDS / L2 round trips, where the register-resident column step is not.
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -34,7 +37,6 @@ namespace xrs {
 namespace {
 
 constexpr int SY_MAX = 256;
-typedef double d4 __attribute__((ext_vector_type(4)));
 
 // Cross-lane sums without the LDS crossbar (a __shfl_xor of a double is two ds_bpermute round trips, the
 // bulk of a column step when chained): DPP row rotations within 16 lanes, v_permlane16_swap across the
@@ -450,40 +452,24 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 // one 64-lane workgroup per wanted eigenvalue: block q -> the q-th largest (ascending index n - 1 - q).
 // Zt (kk x ldz): row q = the eigenvector of T (normalised); lam[q]. status[0] <- -1 if a multisection
 // did not reach full precision.
-//
-// Every O(n) recurrence here is a dependent chain, so the kernel is written for chain latency:
-//  * Sturm counts (multisection, lane l at the point lo + (hi - lo)(l + 1)/65) by the three-term recurrence
-//    p_k = (d_k - x) p_{k-1} - e_{k-1}^2 p_{k-2} (one FMA per level on the chain, instead of a reciprocal
-//    and its Newton steps in the ratio form q_k = p_k / p_{k-1}); #{lambda < x} = sign changes of p_0..p_n
-//    (Barth, Martin & Wilkinson), an exact zero p_k taken as q_k = -pivmin (dlaebz's rule), the pair
-//    (p_{k-1}, p_k) rescaled by a power of two every 8 levels (no over/underflow, signs unchanged). The
-//    operands are uniform across lanes: blocks of 8 are read from LDS one block ahead of the chain.
-//  * inverse iteration: the partially pivoted LU of T - lambda I (dgttrf) as a streaming recurrence whose
-//    running pivot row stays in registers (factors stored to LDS, off the chain), the solves (dgttrs) with
-//    their operands prefetched a block ahead. (The first version kept every running value in LDS: each
-//    level waited on LDS round trips, ~100 us per eigenvalue set at n = 128.)
 template <int NEWTON>
 __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
                                                      double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status) {
-    constexpr int B8 = 8;
-    __shared__ double sd[SY_MAX + 2 * B8], se[SY_MAX + 2 * B8], se2[SY_MAX + 2 * B8];
-    __shared__ double ud[SY_MAX], uu[SY_MAX], uu2[SY_MAX], ul[SY_MAX], lb[SY_MAX];
-    __shared__ int upv[SY_MAX];
+    __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX];
+    __shared__ double ld[SY_MAX], ldl[SY_MAX], ldu[SY_MAX], ldu2[SY_MAX], lb[SY_MAX];
+    __shared__ int lpiv[SY_MAX];
     const int lane = threadIdx.x, q = blockIdx.x, m = n - 1 - q;
     double gl = 1e300, gu = -1e300, emax2 = 0.0, amax = 0.0;
-    for (int i = lane; i < n + 2 * B8; i += 64) {
-        const bool in = i < n;
-        const double di = in ? d[i] : 0.0, ei = i + 1 < n ? e[i] : 0.0, em = (in && i > 0) ? e[i - 1] : 0.0;
+    for (int i = lane; i < n; i += 64) {
+        const double di = d[i], ei = i + 1 < n ? e[i] : 0.0, em = i > 0 ? e[i - 1] : 0.0;
         sd[i] = di;
         se[i] = ei;
         se2[i] = ei * ei;
-        if (in) {
-            const double r = fabs(ei) + fabs(em);
-            gl = fmin(gl, di - r);
-            gu = fmax(gu, di + r);
-            emax2 = fmax(emax2, ei * ei);
-            amax = fmax(amax, fabs(di) + r);
-        }
+        const double r = fabs(ei) + fabs(em);
+        gl = fmin(gl, di - r);
+        gu = fmax(gu, di + r);
+        emax2 = fmax(emax2, ei * ei);
+        amax = fmax(amax, fabs(di) + r);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -492,20 +478,6 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         emax2 = fmax(emax2, __shfl_xor(emax2, o, 64));
         amax = fmax(amax, __shfl_xor(amax, o, 64));
     }
-    // T scaled by a power of two to ||T|| ~ 1 (the recurrences then neither overflow nor underflow within
-    // their 8-level rescaling blocks); the eigenvalue is scaled back, the eigenvector is unaffected
-    const int tex = amax > 0.0 ? __builtin_amdgcn_frexp_exp(amax) : 0;
-    const double tsc = __builtin_amdgcn_ldexp(1.0, -tex);
-    __syncthreads();
-    for (int i = lane; i < n; i += 64) {
-        sd[i] *= tsc;
-        se[i] *= tsc;
-        se2[i] *= tsc * tsc;
-    }
-    gl *= tsc;
-    gu *= tsc;
-    emax2 *= tsc * tsc;
-    amax *= tsc;
     __syncthreads();
     const double pivmin = 1e-290 * fmax(1.0, emax2);
     const double span = fmax(gu - gl, 1e-300);
@@ -515,38 +487,13 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     bool done = false;
     for (; rounds < 16 && !done; ++rounds) {
         const double x = lo + (hi - lo) * double(lane + 1) * (1.0 / 65.0);
-        double pm = 1.0, p = sd[0] - x;   // p_0 = 1, p_1 = d_0 - x
-        if (p == 0.0) p = -pivmin;
-        int c = p < 0.0;
-        double dn[B8], en[B8];
-#pragma unroll
-        for (int u = 0; u < B8; ++u) {
-            dn[u] = sd[1 + u];
-            en[u] = se2[u];
-        }
-        for (int i0 = 1; i0 < n; i0 += B8) {
-            double dc[B8], ec[B8];
-#pragma unroll
-            for (int u = 0; u < B8; ++u) {
-                dc[u] = dn[u];
-                ec[u] = en[u];
-                dn[u] = sd[i0 + B8 + u];   // next block (padded: reads stay inside the arrays)
-                en[u] = se2[i0 + B8 - 1 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < B8; ++u) {
-                if (i0 + u < n) {
-                    double pn = fma(dc[u] - x, p, -ec[u] * pm);
-                    if (pn == 0.0) pn = -pivmin * p;
-                    c += (pn < 0.0) != (p < 0.0);
-                    pm = p;
-                    p = pn;
-                }
-            }
-            // rescale the pair by a power of two (signs and ratios unchanged)
-            const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(p), fabs(pm)));
-            p = __builtin_amdgcn_ldexp(p, -ex);
-            pm = __builtin_amdgcn_ldexp(pm, -ex);
+        double qv = sd[0] - x;
+        if (fabs(qv) < pivmin) qv = -pivmin;
+        int c = qv < 0.0;
+        for (int i = 1; i < n; ++i) {
+            qv = (sd[i] - x) - se2[i - 1] * rcpn<NEWTON>(qv);
+            if (fabs(qv) < pivmin) qv = -pivmin;
+            c += qv < 0.0;
         }
         double nlo = c <= m ? x : -1e300, nhi = c >= m + 1 ? x : 1e300;
 #pragma unroll
@@ -560,120 +507,72 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         done = (hi - lo) <= 2.2204460492503131e-16 * (2.0 * fmax(fabs(lo), fabs(hi)) + 4.0 * span) + 2.0 * pivmin;
     }
     const double lmb = 0.5 * (lo + hi);
-    const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
+    __shared__ double ild[SY_MAX];   // inverse pivots of U
     if (lane == 0) {
-        lam[q] = __builtin_amdgcn_ldexp(lmb, tex);
+        lam[q] = lmb;
         if (!done) atomicMin(status, -1);
-        // LU of T - lambda I with row interchanges where the subdiagonal entry is larger (dgttrf); the
-        // running pivot row (a, b) = (diagonal, superdiagonal) of row i after the earlier eliminations.
-        // Outputs per row: U diagonal ud (tiny pivots replaced by u ||T||, dlagtf's perturbation, stored
-        // inverted), U super- / second superdiagonal uu, uu2, multiplier ul, interchange flag upv.
-        double a = sd[0] - lmb, b = se[0];
-        double sub[B8], dnx[B8], unx[B8];
-#pragma unroll
-        for (int u = 0; u < B8; ++u) {
-            sub[u] = se[u];
-            dnx[u] = sd[1 + u] - lmb;
-            unx[u] = se[1 + u];
+        // inverse iteration: T - lambda I = P L U (dgttrf, row interchanges where the subdiagonal entry is
+        // larger), tiny pivots replaced by u ||T|| (dlagtf's perturbation)
+        for (int i = 0; i < n; ++i) {
+            ld[i] = sd[i] - lmb;
+            ldl[i] = i + 1 < n ? se[i] : 0.0;
+            ldu[i] = i + 1 < n ? se[i] : 0.0;
+            ldu2[i] = 0.0;
+            lpiv[i] = i;
         }
-        for (int i0 = 0; i0 + 1 < n; i0 += B8) {
-            double s_[B8], dx[B8], ux[B8];
-#pragma unroll
-            for (int u = 0; u < B8; ++u) {
-                s_[u] = sub[u];
-                dx[u] = dnx[u];
-                ux[u] = unx[u];
-                sub[u] = se[i0 + B8 + u];
-                dnx[u] = sd[i0 + B8 + 1 + u] - lmb;
-                unx[u] = se[i0 + B8 + 1 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < B8; ++u) {
-                const int i = i0 + u;
-                if (i + 1 < n) {
-                    if (fabs(a) >= fabs(s_[u])) {   // no interchange
-                        const double f = a != 0.0 ? s_[u] * rcpn<NEWTON>(a) : 0.0;
-                        ud[i] = a;
-                        uu[i] = b;
-                        uu2[i] = 0.0;
-                        ul[i] = f;
-                        upv[i] = 0;
-                        a = fma(-f, b, dx[u]);
-                        b = ux[u];
-                    } else {                        // rows i and i+1 interchanged
-                        const double f = a * rcpn<NEWTON>(s_[u]);
-                        ud[i] = s_[u];
-                        uu[i] = dx[u];
-                        uu2[i] = i + 2 < n ? ux[u] : 0.0;
-                        ul[i] = f;
-                        upv[i] = 1;
-                        a = fma(-f, dx[u], b);
-                        b = i + 2 < n ? -f * ux[u] : 0.0;
-                    }
+        for (int i = 0; i + 1 < n; ++i) {
+            if (fabs(ld[i]) >= fabs(ldl[i])) {
+                if (ld[i] != 0.0) {
+                    const double f = ldl[i] * rcpn<NEWTON>(ld[i]);
+                    ldl[i] = f;
+                    ld[i + 1] -= f * ldu[i];
                 }
+            } else {
+                const double f = ld[i] * rcpn<NEWTON>(ldl[i]);
+                ld[i] = ldl[i];
+                ldl[i] = f;
+                const double tmp = ldu[i];
+                ldu[i] = ld[i + 1];
+                ld[i + 1] = tmp - f * ld[i + 1];
+                if (i + 2 < n) {
+                    ldu2[i] = ldu[i + 1];
+                    ldu[i + 1] = -f * ldu[i + 1];
+                }
+                lpiv[i] = i + 1;
             }
         }
-        ud[n - 1] = a;
     }
     __syncthreads();
-    for (int i = lane; i < n; i += 64) {
-        double p = ud[i];
-        if (fabs(p) < tiny) p = copysign(tiny, p == 0.0 ? 1.0 : p);
-        ud[i] = rcp2(p);   // inverse pivots
-        lb[i] = 1.0 + double((i * 37 + q * 11) % 17) * (1.0 / 17.0);
+    {
+        const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
+        for (int i = lane; i < n; i += 64) {
+            double p = ld[i];
+            if (fabs(p) < tiny) p = copysign(tiny, p == 0.0 ? 1.0 : p);
+            ild[i] = rcp2(p);
+            lb[i] = 1.0 + double((i * 37 + q * 11) % 17) * (1.0 / 17.0);
+        }
     }
     __syncthreads();
     for (int it = 0; it < 3; ++it) {
-        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution, operands a block ahead
+        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in registers)
             double cur = lb[0];
-            for (int i0 = 0; i0 + 1 < n; i0 += B8) {
-                double f[B8], nx[B8];
-                int pv[B8];
-#pragma unroll
-                for (int u = 0; u < B8; ++u) {
-                    const int i = i0 + u;
-                    const bool in = i + 1 < n;
-                    f[u] = in ? ul[i] : 0.0;
-                    nx[u] = in ? lb[i + 1] : 0.0;
-                    pv[u] = in ? upv[i] : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < B8; ++u) {
-                    const int i = i0 + u;
-                    if (i + 1 < n) {
-                        if (pv[u] == 0) {
-                            lb[i] = cur;
-                            cur = fma(-f[u], cur, nx[u]);
-                        } else {
-                            lb[i] = nx[u];
-                            cur = fma(-f[u], nx[u], cur);
-                        }
-                    }
+            for (int i = 0; i + 1 < n; ++i) {
+                const double nxt = lb[i + 1], f = ldl[i];
+                if (lpiv[i] == i) {
+                    lb[i] = cur;
+                    cur = fma(-f, cur, nxt);
+                } else {
+                    lb[i] = nxt;
+                    cur = fma(-f, nxt, cur);
                 }
             }
-            double x1 = cur * ud[n - 1], x2 = 0.0;
+            double x1 = cur * ild[n - 1], x2 = 0.0;
             lb[n - 1] = x1;
-            for (int i1 = n - 2; i1 >= 0; i1 -= B8) {
-                double rb[B8], u1[B8], u2[B8], iv[B8];
-#pragma unroll
-                for (int u = 0; u < B8; ++u) {
-                    const int i = i1 - u;
-                    const bool in = i >= 0;
-                    rb[u] = in ? lb[i] : 0.0;
-                    u1[u] = in ? uu[i] : 0.0;
-                    u2[u] = in ? uu2[i] : 0.0;
-                    iv[u] = in ? ud[i] : 0.0;
-                }
-#pragma unroll
-                for (int u = 0; u < B8; ++u) {
-                    const int i = i1 - u;
-                    if (i >= 0) {
-                        const double x0 = fma(-u1[u], x1, fma(-u2[u], x2, rb[u])) * iv[u];
-                        lb[i] = x0;
-                        x2 = x1;
-                        x1 = x0;
-                    }
-                }
+            for (int i = n - 2; i >= 0; --i) {
+                const double x0 = (lb[i] - ldu[i] * x1 - ldu2[i] * x2) * ild[i];
+                lb[i] = x0;
+                x2 = x1;
+                x1 = x0;
             }
         }
         __syncthreads();
@@ -750,414 +649,6 @@ __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, con
     }
 }
 
-__global__ void k_sqrt_lam(const double* __restrict__ lam, int kk, double* __restrict__ S) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kk) S[i] = sqrt(fmax(lam[i], 0.0));
-}
-
-// ---------------------------------------------------------------------------------------------------------
-// Two-stage tridiagonalisation (orders 33..256): dense -> band of width SB by blocked Householder panels
-// whose two-sided trailing updates are MFMA products (k_sy2sb), then band -> tridiagonal by bulge chasing
-// with one wave per sweep and the sweeps pipelined across the workgroup's waves (k_sb2st). The one-stage
-// kernels above spend every column step on a workgroup-wide latency chain (3 barriers, ~3 us per column);
-// here the dense work is blocked (16 columns per panel, one chain of MFMA launches per panel) and the
-// column-by-column work runs on 16 x 16 blocks inside single waves. Back-transformation: the stage-2
-// reflectors by wavefront-parallel application (k_apply_q2), the panel reflectors as block reflectors
-// I - V T V^T with MFMA (k_apply_q1).
-constexpr int SB = 16;              // band width
-constexpr int AB_LD = 2 * SB;       // band + bulge storage per column in k_sb2st
-constexpr int SB_WAVES = 8;         // waves of k_sb2st (concurrent sweeps)
-
-__device__ __forceinline__ void wave_lds_order() { __builtin_amdgcn_wave_barrier(); __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront"); }
-
-struct Sy2sbArgs {
-    const double* A;   // input, lower triangle read (lda)
-    int lda, n;
-    double* W;         // n x n work matrix (lower triangle maintained)
-    double* band;      // (SB + 1) x n: band[k n + j] = A[j + k][j]
-    double* V;         // panel p's reflectors (m_p x SB, row-major) at p * SB * n
-    double* T;         // panel p's block-reflector factor (SB x SB upper) at p * SB * SB
-};
-
-// stage 1: A = Q1 Bd Q1^T, Q1 = prod_p (I - V_p T_p V_p^T) acting on rows r0_p = SB (p + 1) .. n-1
-__global__ void __launch_bounds__(256) k_sy2sb(const Sy2sbArgs g) {
-    __shared__ double Vs[SY_MAX * SB], Xs[SY_MAX * SB], Ws[SY_MAX * SB];
-    __shared__ double Gp[4][SB * SB], Ts[SB * SB], Zs[SB * SB];
-    __shared__ double vcol[2][SY_MAX], taus[SB];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int n = g.n;
-    double* __restrict__ W = g.W;
-    for (int e = tid; e < n * n; e += 256) {
-        const int r = e / n, c = e - r * n;
-        if (c <= r) W[e] = g.A[size_t(r) * g.lda + c];
-    }
-    __syncthreads();
-    for (int p = 0;; ++p) {
-        const int c0 = SB * p, r0 = c0 + SB, m = n - r0;
-        {   // the diagonal block of the band is final (later panels touch rows / columns >= r0 only)
-            const int r = tid >> 4, c = tid & 15;
-            if (c0 + r < n && c <= r) g.band[(r - c) * n + c0 + c] = W[(c0 + r) * n + c0 + c];
-        }
-        if (m < 2) {   // nothing left to annihilate (a single row below is inside the band)
-            if (m == 1) {
-                if (tid < SB) g.band[(SB - tid) * n + c0 + tid] = W[(n - 1) * n + c0 + tid];
-                if (tid == 0) g.band[n - 1] = W[(n - 1) * n + n - 1];
-            }
-            break;
-        }
-        const int MT = (m + SB - 1) / SB, KS = (m + 3) / 4;
-        // (1) panel QR, m x SB: wave w holds columns 4w .. 4w+3 of rows lane + 64 t
-        double P[4][4];
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int i = lane + 64 * t;
-                P[t][cc] = i < m ? W[(r0 + i) * n + c0 + 4 * wave + cc] : 0.0;
-            }
-#pragma unroll
-        for (int j = 0; j < SB; ++j) {
-            const int jc = j & 3;
-            double* vc = vcol[j & 1];   // double-buffered: one barrier per column
-            if (wave == (j >> 2)) {     // dlarfg on column j
-                const double alpha = __shfl(P[0][jc], j, 64);
-                double s = 0.0;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int i = lane + 64 * t;
-                    if (i > j && i < m) s = fma(P[t][jc], P[t][jc], s);
-                }
-                s = sum64(s);
-                double tv = 0.0, beta = alpha, scal = 0.0;
-                if (s > 0.0) {
-                    beta = -copysign(sqrt(fma(alpha, alpha, s)), alpha);
-                    tv = (beta - alpha) * rcp2(beta);
-                    scal = rcp2(alpha - beta);
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int i = lane + 64 * t;
-                    const double v = (i < j || i >= m) ? 0.0 : (i == j ? 1.0 : P[t][jc] * scal);
-                    vc[i] = v;
-                    Vs[i * SB + j] = v;
-                    if (i == j) P[t][jc] = beta;
-                    else if (i > j) P[t][jc] = 0.0;
-                }
-                if (lane == 0) taus[j] = tv;
-            }
-            __syncthreads();
-            const double tj = taus[j];
-            if (4 * wave + 3 > j && tj != 0.0) {   // H_j on the wave's columns right of j
-                double dots[4], vv[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) vv[t] = vc[lane + 64 * t];
-#pragma unroll
-                for (int cc = 0; cc < 4; ++cc) {
-                    double a = 0.0;
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) a = fma(vv[t], P[t][cc], a);
-                    dots[cc] = (4 * wave + cc > j) ? sum64(a) : 0.0;
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-#pragma unroll
-                    for (int cc = 0; cc < 4; ++cc)
-                        if (4 * wave + cc > j) P[t][cc] = fma(-tj * dots[cc], vv[t], P[t][cc]);
-            }
-        }
-        // R (rows 0..15 of the panel, lanes 0..15) into the band; V to global for the back-transformation
-        if (lane < SB && lane < m) {
-#pragma unroll
-            for (int cc = 0; cc < 4; ++cc) {
-                const int c = 4 * wave + cc;
-                if (c >= lane) g.band[(SB + lane - c) * n + c0 + c] = P[0][cc];
-            }
-        }
-        for (int e = tid; e < m * SB; e += 256) g.V[size_t(p) * SB * n + e] = Vs[e];
-        // (2) T (dlarft, forward columnwise) from G = V^T V (MFMA, K split over the waves)
-        {
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-            for (int ks = wave; ks < KS; ks += 4) {
-                const double v = Vs[(4 * ks + (lane >> 4)) * SB + (lane & 15)];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(v, v, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Gp[wave][((lane >> 4) + 4 * q) * SB + (lane & 15)] = acc[q];
-        }
-        __syncthreads();
-        if (wave == 0 && lane < SB) {
-            const int i = lane;
-            double trow[SB];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                double s = 0.0;
-#pragma unroll
-                for (int k = 0; k < j; ++k) {
-                    const double gkj = (Gp[0][k * SB + j] + Gp[1][k * SB + j]) + (Gp[2][k * SB + j] + Gp[3][k * SB + j]);
-                    if (k >= i) s = fma(trow[k], gkj, s);
-                }
-                trow[j] = (i == j) ? taus[j] : (i < j ? -taus[j] * s : 0.0);
-            }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                Ts[i * SB + j] = trow[j];
-                g.T[p * SB * SB + i * SB + j] = trow[j];
-            }
-        }
-        __syncthreads();
-        // (3) X = A22 V (A22: rows / columns r0.., symmetric reads of the lower triangle), MFMA tiles
-        for (int I = wave; I < MT; I += 4) {
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-            const int ra = SB * I + (lane & 15);
-            for (int J = 0; J < MT; ++J) {
-                double av[4], bv[4];
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    const int ca = SB * J + 4 * ks + (lane >> 4);
-                    const int hi = ra > ca ? ra : ca, lo = ra > ca ? ca : ra;
-                    av[ks] = (hi < m) ? W[(r0 + hi) * n + r0 + lo] : 0.0;
-                    bv[ks] = Vs[ca * SB + (lane & 15)];
-                }
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ks], bv[ks], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Xs[(SB * I + (lane >> 4) + 4 * q) * SB + (lane & 15)] = acc[q];
-        }
-        __syncthreads();
-        // (4) Y = X T (in place, one row per thread), S = V^T Y, Z = T^T S, W = Y - V Z / 2
-        if (tid < SB * MT) {
-            double x[SB], y[SB];
-#pragma unroll
-            for (int k = 0; k < SB; ++k) x[k] = Xs[tid * SB + k];
-#pragma unroll
-            for (int c = 0; c < SB; ++c) {
-                double a = 0.0;
-#pragma unroll
-                for (int k = 0; k <= c; ++k) a = fma(x[k], Ts[k * SB + c], a);
-                y[c] = a;
-            }
-#pragma unroll
-            for (int c = 0; c < SB; ++c) Xs[tid * SB + c] = y[c];
-        }
-        __syncthreads();
-        {
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-            for (int ks = wave; ks < KS; ks += 4) {
-                const int k = 4 * ks + (lane >> 4);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Vs[k * SB + (lane & 15)], Xs[k * SB + (lane & 15)], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Gp[wave][((lane >> 4) + 4 * q) * SB + (lane & 15)] = acc[q];
-        }
-        __syncthreads();
-        {
-            const int a = tid >> 4, c = tid & 15;
-            double z = 0.0;
-            for (int k = 0; k <= a; ++k) {
-                const double skc = (Gp[0][k * SB + c] + Gp[1][k * SB + c]) + (Gp[2][k * SB + c] + Gp[3][k * SB + c]);
-                z = fma(Ts[k * SB + a], skc, z);
-            }
-            Zs[a * SB + c] = z;
-        }
-        __syncthreads();
-        if (tid < SB * MT) {
-            double v[SB];
-#pragma unroll
-            for (int k = 0; k < SB; ++k) v[k] = Vs[tid * SB + k];
-#pragma unroll
-            for (int c = 0; c < SB; ++c) {
-                double a = 0.0;
-#pragma unroll
-                for (int k = 0; k < SB; ++k) a = fma(v[k], Zs[k * SB + c], a);
-                Ws[tid * SB + c] = fma(-0.5, a, Xs[tid * SB + c]);
-            }
-        }
-        __syncthreads();
-        // (5) A22 -= V W^T + W V^T on the lower tiles (MFMA, C layout: row (l >> 4) + 4 q, column l & 15)
-        const int ntl = MT * (MT + 1) / 2;
-        for (int tile = wave; tile < ntl; tile += 4) {
-            int I = int((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-            while ((I + 1) * (I + 2) / 2 <= tile) ++I;
-            while (I * (I + 1) / 2 > tile) --I;
-            const int J = tile - I * (I + 1) / 2;
-            const int cj = SB * J + (lane & 15);
-            d4 acc;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int ri = SB * I + (lane >> 4) + 4 * q;
-                acc[q] = (ri < m && cj < m && ri >= cj) ? W[(r0 + ri) * n + r0 + cj] : 0.0;
-            }
-            const int ar = (SB * I + (lane & 15)) * SB, br = (SB * J + (lane & 15)) * SB;
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const int k = 4 * ks + (lane >> 4);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Vs[ar + k], Ws[br + k], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-Ws[ar + k], Vs[br + k], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int ri = SB * I + (lane >> 4) + 4 * q;
-                if (ri < m && cj < m && ri >= cj) W[(r0 + ri) * n + r0 + cj] = acc[q];
-            }
-        }
-        __syncthreads();
-    }
-}
-
-// stage 2: band (width SB, lower storage) -> tridiagonal by bulge chasing (sweep s annihilates column s;
-// its block k >= 1 applies the previous reflector from the right to the block below (creating the bulge),
-// annihilates the bulge's first column with a new reflector from the left, and applies that reflector to
-// the next diagonal block from both sides). One wave per sweep (a 16 x 16 block: lane l holds row l & 15,
-// columns (l >> 4) + 4 t); sweep s waits until sweep s - 1 has finished two more blocks than it is about to
-// start (the blocks that overlap). Reflector (s, k) -> refl[((2 s + k) nslot + k / 2) 17]: v[0..15], tau
-// (grouped by the wavefront t = 2 s + k: the reflectors of one t act on disjoint rows, see k_apply_q2).
-__global__ void __launch_bounds__(SB_WAVES * 64) k_sb2st(const double* __restrict__ band, int n, double* __restrict__ d,
-                                                        double* __restrict__ e, double* __restrict__ refl, int nslot) {
-    __shared__ double ab[SY_MAX * AB_LD];
-    __shared__ int prog[SY_MAX];
-    __shared__ double sv[SB_WAVES][SB], sw[SB_WAVES][SB], sx[SB_WAVES][SB];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (int q = tid; q < n * AB_LD; q += SB_WAVES * 64) {
-        const int j = q / AB_LD, k = q - j * AB_LD;
-        ab[q] = (k <= SB && j + k < n) ? band[k * n + j] : 0.0;
-    }
-    for (int q = tid; q < SY_MAX; q += SB_WAVES * 64) prog[q] = 0;
-    __syncthreads();
-    const int r = lane & 15, gq = lane >> 4;
-    double* vsh = sv[wave];
-    double* wsh = sw[wave];
-    double* xsh = sx[wave];
-    // A[row][col] of the lower band + bulge (row >= col, row - col < AB_LD)
-    auto at = [&](int row, int col) -> double& { return ab[col * AB_LD + (row - col)]; };
-    // two-sided H D H on the symmetric block rows / columns i0 .. i0+L-1, H = I - tau v v^T (v_r in vsh)
-    auto two_sided = [&](int i0, int L, double tau) {
-        if (tau == 0.0) return;
-        double D[4], vc[4];
-        const bool rin = r < L;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int c = gq + 4 * t;
-            vc[t] = vsh[c];
-            D[t] = (rin && c < L) ? (r >= c ? at(i0 + r, i0 + c) : at(i0 + c, i0 + r)) : 0.0;
-        }
-        const double vr = vsh[r];
-        double pr = (D[0] * vc[0] + D[1] * vc[1]) + (D[2] * vc[2] + D[3] * vc[3]);
-        pr += xor16(pr);
-        pr += xor32(pr);
-        pr *= tau;
-        const double K = -0.5 * tau * sum16(pr * vr);
-        const double wr = fma(K, vr, pr);
-        if (gq == 0) wsh[r] = wr;
-        wave_lds_order();
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int c = gq + 4 * t;
-            const double wc = wsh[c];
-            const double u = fma(-vr, wc, fma(-wr, vc[t], D[t]));
-            if (rin && c < L && r >= c) at(i0 + r, i0 + c) = u;
-        }
-        wave_lds_order();
-    };
-    for (int s = wave; s + 2 < n; s += SB_WAVES) {
-        const int nblk = (n - 2 - s) / SB + 1;
-        double tprev = 0.0;
-        int Lprev = 0;
-        for (int k = 0; k < nblk; ++k) {
-            if (s > 0) {   // sweep s - 1 two blocks ahead (or finished)
-                while (__hip_atomic_load(&prog[s - 1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < k + 2)
-                    __builtin_amdgcn_s_sleep(1);
-            }
-            double tau;
-            int L;
-            if (k == 0) {   // annihilate column s below its subdiagonal
-                L = min(SB, n - 1 - s);
-                const double x = r < L ? at(s + 1 + r, s) : 0.0;
-                const double alpha = __shfl(x, 0, 16);
-                const double ss = sum16(r >= 1 ? x * x : 0.0);
-                double beta = alpha, scal = 0.0;
-                tau = 0.0;
-                if (ss > 0.0) {
-                    beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-                    tau = (beta - alpha) * rcp2(beta);
-                    scal = rcp2(alpha - beta);
-                }
-                const double v = r == 0 ? 1.0 : (r < L ? x * scal : 0.0);
-                if (gq == 0) {
-                    vsh[r] = v;
-                    if (r < L && tau != 0.0) at(s + 1 + r, s) = r == 0 ? beta : 0.0;
-                }
-                wave_lds_order();
-                two_sided(s + 1, L, tau);
-            } else {
-                const int R0 = s + 1 + k * SB, C0 = R0 - SB;
-                L = min(SB, n - R0);
-                // C = A[R0 .., C0 ..] (L x Lprev): C <- C H_{k-1}, then H_k from C's first column, C <- H_k C
-                double C[4], vc[4];
-                const bool rin = r < L;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int c = gq + 4 * t;
-                    vc[t] = vsh[c];
-                    C[t] = (rin && c < Lprev) ? at(R0 + r, C0 + c) : 0.0;
-                }
-                if (tprev != 0.0) {
-                    double y = (C[0] * vc[0] + C[1] * vc[1]) + (C[2] * vc[2] + C[3] * vc[3]);
-                    y += xor16(y);
-                    y += xor32(y);
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) C[t] = fma(-tprev * y, vc[t], C[t]);
-                }
-                if (gq == 0) xsh[r] = C[0];   // the first column (c = 0 on the lanes with gq = 0, t = 0)
-                wave_lds_order();
-                const double x = xsh[r];
-                const double alpha = xsh[0];
-                const double ss = sum16(r >= 1 && rin ? x * x : 0.0);
-                double beta = alpha, scal = 0.0;
-                tau = 0.0;
-                if (ss > 0.0) {
-                    beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
-                    tau = (beta - alpha) * rcp2(beta);
-                    scal = rcp2(alpha - beta);
-                }
-                const double vr = r == 0 ? 1.0 : (rin ? x * scal : 0.0);
-                if (tau != 0.0) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const double z = sum16(vr * C[t]);
-                        C[t] = fma(-tau * z, vr, C[t]);
-                    }
-                    if (gq == 0) C[0] = r == 0 ? beta : 0.0;
-                }
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int c = gq + 4 * t;
-                    if (rin && c < Lprev) at(R0 + r, C0 + c) = C[t];
-                }
-                wave_lds_order();
-                if (gq == 0) vsh[r] = vr;
-                wave_lds_order();
-                two_sided(R0, L, tau);
-            }
-            if (refl) {   // reflector (s, k) for the back-transformation, at wavefront t = 2 s + k, slot k / 2
-                double* rp = refl + (size_t(2 * s + k) * nslot + (k >> 1)) * 17;
-                if (gq == 0) rp[r] = vsh[r];
-                if (lane == 0) rp[16] = tau;
-            }
-            tprev = tau;
-            Lprev = L;
-            wave_lds_order();
-            if (lane == 0) __hip_atomic_store(&prog[s], k + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if (lane == 0) __hip_atomic_store(&prog[s], 1 << 30, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    __syncthreads();
-    for (int j = tid; j < n; j += SB_WAVES * 64) {
-        d[j] = at(j, j);
-        if (j + 1 < n) e[j] = at(j + 1, j);
-    }
-}
-
 // Clusters of close eigenvalues (|lam_i - lam_{i+1}| <= 1e-3 ||T||, dstein's ORTOL): inverse iteration from
 // different start vectors lands in the cluster's invariant subspace, but not orthogonally -- the vectors of each
 // cluster are orthonormalised by two passes of modified Gram-Schmidt (in order of decreasing eigenvalue, as
@@ -1209,125 +700,9 @@ __global__ void __launch_bounds__(256) k_cluster_orth(const double* __restrict__
     }
 }
 
-// Q2 z for the kk eigenvectors z of T (rows of Zt, in place): the stage-2 reflectors in reverse order of
-// generation. Sweep s's block k acts on rows s + 1 + 16 k .. +15; the reflectors of one wavefront t = 2 s + k
-// act on disjoint rows (consecutive sweeps' blocks of equal t are 2 SB - 1 rows apart) and, whenever an
-// earlier-generated reflector has a larger t, the two are disjoint too -- so applying the wavefronts from the
-// last to the first, each wavefront's reflectors in any order, is the reverse generation order. The
-// reflectors are shared by all vectors: chunks of QC_T wavefronts are staged through LDS by the workgroup;
-// each wave carries one vector (LDS), its 4 groups of 16 lanes apply a wavefront's reflectors (one per row
-// of 16 lanes: a DPP row sum and one FMA), no barriers inside a chunk.
-constexpr int QC_T = 32;
-template <int NSLOT>
-__global__ void __launch_bounds__(256) k_apply_q2(const double* __restrict__ refl, int n, int kk, int tcount, double* __restrict__ Zt,
-                                                  int ldz) {
-    __shared__ double rs[QC_T * NSLOT * 17];
-    __shared__ double zs[4][SY_MAX];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int r = lane & 15, g = lane >> 4;
-    const int q = blockIdx.x * 4 + wave;
-    const bool live = q < kk;
-    for (int i = lane; i < n; i += 64) zs[wave][i] = live ? Zt[size_t(q) * ldz + i] : 0.0;
-    double* z = zs[wave];
-    for (int thi = tcount - 1; thi >= 0; thi -= QC_T) {
-        const int tlo = max(0, thi - QC_T + 1);
-        __syncthreads();
-        const int cnt = (thi - tlo + 1) * NSLOT * 17;
-        for (int e = tid; e < cnt; e += 256) rs[e] = refl[size_t(tlo) * NSLOT * 17 + e];
-        __syncthreads();
-        for (int t = thi; t >= tlo; --t) {
-            const double* rt = rs + (t - tlo) * NSLOT * 17;
-            double zr[(NSLOT + 3) / 4], vr[(NSLOT + 3) / 4], tr[(NSLOT + 3) / 4];
-            int row[(NSLOT + 3) / 4];
-#pragma unroll
-            for (int u = 0; u < (NSLOT + 3) / 4; ++u) {   // the group's reflectors of this wavefront (disjoint rows)
-                const int slot = g + 4 * u;
-                const int k = 2 * slot + (t & 1), s = (t - k) >> 1;
-                const int R0 = s + 1 + SB * k;
-                const bool ok = slot < NSLOT && k <= t && R0 + r < n;
-                row[u] = ok ? R0 + r : -1;
-                vr[u] = ok ? rt[slot * 17 + r] : 0.0;
-                tr[u] = ok ? rt[slot * 17 + 16] : 0.0;
-                zr[u] = ok ? z[R0 + r] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < (NSLOT + 3) / 4; ++u) {
-                const double dot = sum16(vr[u] * zr[u]);
-                if (row[u] >= 0) z[row[u]] = fma(-tr[u] * dot, vr[u], zr[u]);
-            }
-            wave_lds_order();
-        }
-    }
-    wave_lds_order();
-    if (live)
-        for (int i = lane; i < n; i += 64) Zt[size_t(q) * ldz + i] = z[i];
-}
-
-// Q1 Y for 16 vectors per workgroup (rows of Zt): the stage-1 block reflectors H_p = I - V_p T_p V_p^T (rows
-// r0_p = 16 (p + 1) ..), applied from the last panel to the first; in row form Y <- Y - ((Y V) T^T) V^T with
-// MFMA: G = Y V (16 x 16, K = m over the 4 waves), G2 = G T^T, then the 16 x m update in 16 x 16 tiles.
-__global__ void __launch_bounds__(256) k_apply_q1(const double* __restrict__ V, const double* __restrict__ Tp, int n, int npanel, int kk,
-                                                  double* __restrict__ Zt, int ldz) {
-    __shared__ double ys[SB * SY_MAX], vs[SY_MAX * SB], gp[4][SB * SB], g2[SB * SB], ts[SB * SB];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int q0 = blockIdx.x * SB;
-    for (int e = tid; e < SB * n; e += 256) {
-        const int a = e / n, i = e - a * n;
-        ys[a * SY_MAX + i] = (q0 + a < kk) ? Zt[size_t(q0 + a) * ldz + i] : 0.0;
-    }
-    for (int p = npanel - 1; p >= 0; --p) {
-        const int r0 = SB * (p + 1), m = n - r0, KS = (m + 3) / 4;
-        __syncthreads();
-        for (int e = tid; e < KS * 4 * SB; e += 256) vs[e] = e < m * SB ? V[size_t(p) * SB * n + e] : 0.0;
-        ts[tid] = Tp[p * SB * SB + tid];
-        __syncthreads();
-        {   // G = Y[:, r0..] V (16 x 16)
-            d4 acc = {0.0, 0.0, 0.0, 0.0};
-            for (int ks = wave; ks < KS; ks += 4) {
-                const int k = 4 * ks + (lane >> 4);
-                const double av = k < m ? ys[(lane & 15) * SY_MAX + r0 + k] : 0.0;
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, vs[k * SB + (lane & 15)], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) gp[wave][((lane >> 4) + 4 * qq) * SB + (lane & 15)] = acc[qq];
-        }
-        __syncthreads();
-        {   // G2 = G T^T: G2[a][c] = sum_k G[a][k] T[c][k] (T upper: k >= c)
-            const int a = tid >> 4, c = tid & 15;
-            double s2 = 0.0;
-            for (int k = c; k < SB; ++k) {
-                const double gak = (gp[0][a * SB + k] + gp[1][a * SB + k]) + (gp[2][a * SB + k] + gp[3][a * SB + k]);
-                s2 = fma(gak, ts[c * SB + k], s2);
-            }
-            g2[a * SB + c] = s2;
-        }
-        __syncthreads();
-        // Y[:, r0 + 16 J ..] -= G2 V_J^T
-        const int MT = (m + SB - 1) / SB;
-        for (int J = wave; J < MT; J += 4) {
-            d4 acc;
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                const int a = (lane >> 4) + 4 * qq, col = SB * J + (lane & 15);
-                acc[qq] = col < m ? ys[a * SY_MAX + r0 + col] : 0.0;
-            }
-#pragma unroll
-            for (int ks = 0; ks < 4; ++ks) {
-                const int k = 4 * ks + (lane >> 4);
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-g2[(lane & 15) * SB + k], vs[(SB * J + (lane & 15)) * SB + k], acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq) {
-                const int a = (lane >> 4) + 4 * qq, col = SB * J + (lane & 15);
-                if (col < m) ys[a * SY_MAX + r0 + col] = acc[qq];
-            }
-        }
-    }
-    __syncthreads();
-    for (int e = tid; e < SB * n; e += 256) {
-        const int a = e / n, i = e - a * n;
-        if (q0 + a < kk) Zt[size_t(q0 + a) * ldz + i] = ys[a * SY_MAX + i];
-    }
+__global__ void k_sqrt_lam(const double* __restrict__ lam, int kk, double* __restrict__ S) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < kk) S[i] = sqrt(fmax(lam[i], 0.0));
 }
 
 }  // namespace
@@ -1341,21 +716,14 @@ bool sym_eig_top_fits(int n, int kk) {
     return n >= 2 && n <= std::min(nmax, SY_MAX) && kk >= 1 && kk <= n;
 }
 
-// Two-stage tridiagonalisation A = Q1 Q2 T Q2^T Q1^T (d, e of T; the reflectors in the optional buffers:
-// V (n x n), Tp (n / SB x SB x SB), refl (17 x (n - 2) x (n / SB + 1))). Enqueued only.
-constexpr int Q2_SLOTS = 9;   // reflectors per wavefront: k / 2 <= (256 / SB) / 2
-size_t q2_refl_elems(int n) { return size_t(2 * n) * Q2_SLOTS * 17; }
-
-void sym_tridiag_2stage(xrs_handle_t h, const double* A, int lda, int n, double* d, double* e, double* V, double* Tp, double* refl) {
-    XRS_REQUIRE(n >= 2 && n <= SY_MAX, "sym_tridiag_2stage: need 2 <= n <= 256");
-    if (refl) XRS_HIP(hipMemsetAsync(refl, 0, q2_refl_elems(n) * 8, h->stream));
-    DevBuf W(h, size_t(n) * n * 8), band(h, size_t(SB + 1) * n * 8), Vb(h, V ? 0 : size_t(n) * n * 8), Tb(h, Tp ? 0 : size_t(n / SB + 1) * SB * SB * 8);
-    XRS_HIP(hipMemsetAsync(band.d(), 0, size_t(SB + 1) * n * 8, h->stream));
-    Sy2sbArgs g{A, lda, n, W.d(), band.d(), V ? V : Vb.d(), Tp ? Tp : Tb.d()};
-    hipLaunchKernelGGL(k_sy2sb, dim3(1), dim3(256), 0, h->stream, g);
-    check_launch("k_sy2sb");
-    hipLaunchKernelGGL(k_sb2st, dim3(1), dim3(SB_WAVES * 64), 0, h->stream, band.d(), n, d, e, refl, Q2_SLOTS);
-    check_launch("k_sb2st");
+// Householder tridiagonalisation alone (d, e of T; xrs_sym_tridiag). Enqueued only.
+void sym_tridiag(xrs_handle_t h, const double* A, int lda, int n, double* d, double* e) {
+    XRS_REQUIRE(n >= 2 && n <= SY_MAX, "sym_tridiag: need 2 <= n <= 256");
+    DevBuf tbuf(h, size_t(n) * 8), V(h, size_t(n) * n * 8);
+    if (n <= 64) hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
+    else if (n <= 128) hipLaunchKernelGGL((k_sytrd<32, 4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
+    else hipLaunchKernelGGL(k_sytrd_l512, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d());
+    check_launch("k_sytrd");
 }
 
 void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status) {
@@ -1367,28 +735,9 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     DevBuf sb(h, want_stamps ? 768 * 8 : 0);
     unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
     if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 768 * 8, h->stream));
-    if (n > 32) {   // two-stage tridiagonalisation, eigenpairs of T, back-transformation Q1 Q2 z
-        DevBuf Vp(h, size_t(n) * n * 8), Tp(h, size_t(n / SB + 1) * SB * SB * 8), refl(h, q2_refl_elems(n) * 8);
-        sym_tridiag_2stage(h, A, lda, n, dbuf.d(), ebuf.d(), Vp.d(), Tp.d(), refl.d());
-        hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
-        check_launch("k_stebz_stein");
-        hipLaunchKernelGGL(k_cluster_orth, dim3(1), dim3(256), 0, h->stream, lm, dbuf.d(), ebuf.d(), n, kk, Ut, ldu);
-        check_launch("k_cluster_orth");
-        hipLaunchKernelGGL((k_apply_q2<Q2_SLOTS>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, refl.d(), n, kk, 2 * n, Ut, ldu);
-        check_launch("k_apply_q2");
-        int npanel = 0;
-        while (n - SB * (npanel + 1) >= 2) ++npanel;
-        if (npanel > 0) {
-            hipLaunchKernelGGL(k_apply_q1, dim3((kk + SB - 1) / SB), dim3(256), 0, h->stream, Vp.d(), Tp.d(), n, npanel, kk, Ut, ldu);
-            check_launch("k_apply_q1");
-        }
-        if (S) {
-            hipLaunchKernelGGL(k_sqrt_lam, dim3((kk + 255) / 256), dim3(256), 0, h->stream, lm, kk, S);
-            check_launch("k_sqrt_lam");
-        }
-        return;
-    }
-    // one-stage (orders <= 32): the register-resident column steps
+    // the 1024-thread grid up to 128 (measured faster than 256 threads with 64 elements each: 5.1 vs 5.6 ms
+    // per cfg3 round(64), profiles/r03/sytrd_grid_ab_r03q.txt -- one wave per SIMD is issue-bound in the
+    // update), the 512-thread lower-block grid above
     if (n <= 64) {
         hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
     } else if (n <= 128) {
