@@ -10,9 +10,10 @@ the canonical form, so every step repeats the same work.
 value = algorithmic GFLOP of the step / wall time (SURVEY 8(d) formulas, not hardware counters):
   <x,y>  : sum_k 2 a_x a_y n b_x + 2 a_y n b_x b_y           (zipper)
   round  : sum_edges 6 a n b^2 + 6 b^2 n' c + 22 b^3         (standard two-sweep TT rounding)
-roofline: a second pass of the same K steps with a HIP event pair around every GEMM launch gives the
-average GEMM launch duration (event packets add GPU time between kernels, so that pass is not the
-headline timing; its ms/step is reported as roofline.events_pass_ms_per_step).
+roofline: a second pass of the same K steps with a HIP event pair on every GEMM launch gives the average
+GEMM launch duration (the events are recorded by the dispatch itself, hipExtLaunchKernelGGL; the pass
+serialises the handle's fork lanes, so it is not the headline timing; its ms/step is reported as
+roofline.events_pass_ms_per_step).
 Multi-GPU: one process per GPU; the headline is replicas (every rank its own TT pair, weak scaling, no
 data-path collective). The "cfg5" object adds BASELINE configs[4]: order-16 rank-512 round() sharded
 over all ranks by mode slices (xerus_amd.dist; one r x r all-reduce per edge over RCCL), strong scaling.
@@ -182,7 +183,7 @@ def bench_cfg2(h):
     tf = 2.0 * n ** 3 / (ev["us_per_launch"] * 1e-6) / 1e12
     return {"workload": "A(i,j) = B(i,k) * C(k,j), 1024^3, fp64 MFMA GEMM", "us": round(ev["us_per_launch"], 2),
             "tflops": round(tf, 2), "frac_fp64_peak": round(tf / FP64_MFMA_PEAK_TFLOPS, 3),
-            "timing": "HIP events around the launch, mean of 20"}
+            "timing": "dispatch begin/end events (hipExtLaunchKernelGGL), mean of 20"}
 
 
 def bench_cfg1(xe):
@@ -213,14 +214,26 @@ def bench_permute(h):
     out = []
     for name, dims, shuf in shapes:
         size = int(np.prod(dims))
-        src = h.array(np.arange(size, dtype=np.float64).reshape(dims))
-        dst = h.empty((size,))
-        ev = _events(h, capi.KFAM_PERMUTE, lambda: h.permute(dst, src, dims, shuf), 20)
+        # rotate over enough source / destination pairs that one pass touches >= 1 GiB (the 256 MB
+        # last-level cache cannot serve a launch from the previous pass), at most 64 pairs
+        nbuf = int(min(64, max(1, -(-(1 << 30) // (16 * size)))))
+        base = np.arange(size, dtype=np.float64).reshape(dims)
+        srcs = [h.array(base) for _ in range(nbuf)]
+        dsts = [h.empty((size,)) for _ in range(nbuf)]
+        reps = max(20, nbuf)
+        it = iter(range(10 ** 9))
+
+        def one():
+            i = next(it) % nbuf
+            h.permute(dsts[i], srcs[i], dims, shuf)
+
+        ev = _events(h, capi.KFAM_PERMUTE, one, reps)
         gbs = 16.0 * size / (ev["us_per_launch"] * 1e-6) / 1e9
         out.append({"shape": name, "mbytes": round(16.0 * size / 1e6, 2), "us": round(ev["us_per_launch"], 2),
-                    "gbs": round(gbs, 1), "frac_hbm_peak": round(gbs / HBM_PEAK_GBS, 3)})
-        src.free()
-        dst.free()
+                    "gbs": round(gbs, 1), "frac_hbm_peak": round(gbs / HBM_PEAK_GBS, 3), "buffers_rotated": nbuf,
+                    "timing": "dispatch begin/end events (hipExtLaunchKernelGGL), mean over the rotated launches"})
+        for b in srcs + dsts:
+            b.free()
     return out
 
 
@@ -449,9 +462,10 @@ def main():
         step_seq(timing)
     barrier()
 
-    # Roofline passes: the same K steps again with a HIP event pair around every GEMM launch (on the stream
-    # each launch goes to). The event packets add GPU-side work between kernels, so these passes are kept
-    # out of the headline timing; their wall times are reported beside it. The kernel's roofline comes
+    # Roofline passes: the same K steps again with a HIP event pair on every GEMM launch (the start / stop
+    # events of hipExtLaunchKernelGGL on the stream each launch goes to: the dispatch's own begin / end
+    # timestamps). The fork lanes are serialised while timing, so these passes are kept out of the headline
+    # timing; their wall times are reported beside it. The kernel's roofline comes
     # from the sequential step (<x,y> waited for before the round starts), where a launch does not share
     # the chip with the other operation's kernels; the overlapped step's per-launch figure is reported
     # beside it (its launch durations include that sharing).
@@ -511,9 +525,10 @@ def main():
             "launches_per_step": prof["launches"] / args.steps,
             "avg_launch_us": round(prof["ms"] / launches * 1e3, 3),
             "events_pass": ("sequential step (x.dot(y), then x.round) with the handle's fork lanes serialised onto its main "
-                            "stream while kernels are timed (xrs_prof_begin): each HIP event pair brackets exactly one kernel, "
-                            "so the per-launch durations agree with a rocprofv3 kernel trace of the same pass "
-                            "(tools/roofline_from_trace.py)"),
+                            "stream while kernels are timed (xrs_prof_begin); each GEMM launch records its HIP event pair itself "
+                            "(hipExtLaunchKernelGGL start/stop events = the dispatch's begin/end timestamps, the interval a "
+                            "rocprofv3 kernel trace reports; marker events around a launch add its ~6 us dispatch latency), "
+                            "so the per-launch durations agree with a kernel trace of the same pass (tools/roofline_from_trace.py)"),
             "events_pass_ms_per_step": round(elapsed_ev / args.steps * 1e3, 4),
             "algorithmic_flops_per_launch": prof["flops"] / launches,
             "algorithmic_bytes_per_launch": prof["bytes"] / launches,

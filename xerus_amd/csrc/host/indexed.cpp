@@ -138,6 +138,14 @@ struct Lowered {
 };
 
 Lowered lower(const IndexedProduct& _p) {
+    // an index occurs at most twice over the whole product, traces inside one factor included (the
+    // reference's network assembly rejects E(i2) = A(i1,i1,i2) * B(i2,i2): tensorNetwork.cxx:193-218)
+    {
+        std::map<uint64, size_t> count;
+        for (const IndexedTerm& t : _p.terms)
+            for (const Index& I : t.indices)
+                if (!I.fixed()) XERUS_REQUIRE(++count[I.valueId] <= 2, "Index must not appear three (or more) times.");
+    }
     std::vector<Reduced> terms;
     terms.reserve(_p.terms.size());
     for (const IndexedTerm& t : _p.terms) terms.push_back(reduce_term(t));

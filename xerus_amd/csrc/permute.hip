@@ -10,6 +10,7 @@
 //   (c) when those modes are shorter than a tile, the same transpose between GROUPS of innermost
 //       input / output modes (flattened indices), so small modes still fill whole tiles.
 // Both are HBM-bound: algorithmic bytes = 2 * size * 8.
+#include <hip/hip_ext.h>
 #include <algorithm>
 #include <numeric>
 
@@ -232,9 +233,10 @@ __global__ void __launch_bounds__(256) k_permute_grouped(double* __restrict__ ou
 void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const size_t* dims, const size_t* shuffle) {
     PermPlan p = make_plan(ndim, dims, shuffle);
     if (p.total == 0) return;
-    KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, 2.0 * double(p.total) * 8.0);
+    const double bytes = 2.0 * double(p.total) * 8.0;
     if (p.n <= 1 || p.out_stride[p.n - 1] == 1) {
         if (p.n <= 1) {
+            KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes);
             XRS_HIP(hipMemcpyAsync(out, in, p.total * 8, hipMemcpyDeviceToDevice, h->stream));
             return;
         }
@@ -248,7 +250,8 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
         ra.rows = p.total / ra.L;
         const size_t waves = std::min<size_t>(ra.rows, 256 * 32);
         const unsigned blocks = unsigned((waves + 3) / 4);
-        hipLaunchKernelGGL(k_permute_rows, dim3(blocks), dim3(256), 0, h->stream, out, in, ra);
+        KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes, true);   // the dispatch's own timestamps
+        hipExtLaunchKernelGGL(k_permute_rows, dim3(blocks), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0, out, in, ra);
         check_launch("k_permute_rows");
         return;
     }
@@ -309,7 +312,9 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
             XRS_REQUIRE(tiles < (1ull << 31) && batch < (1ull << 32) && pa < (1ull << 32) && pb < (1ull << 32), "permutation too large");
             // a few batch items per workgroup (the row offsets are computed once per workgroup)
             const unsigned gy = unsigned(std::max<size_t>(1, std::min<size_t>({batch, 65535, (size_t(1) << 13) / tiles})));
-            hipLaunchKernelGGL(k_permute_grouped, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, out, in, g, batch);
+            KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes, true);
+            hipExtLaunchKernelGGL(k_permute_grouped, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0,
+                                  out, in, g, batch);
             check_launch("k_permute_grouped");
             return;
         }
@@ -334,7 +339,9 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
     const size_t tiles = size_t(ta.tiles_a) * ta.tiles_b;
     XRS_REQUIRE(tiles < (1ull << 31) && batch < (1ull << 32), "permutation too large");
     const unsigned gy = unsigned(std::min<size_t>(batch, 65535));
-    hipLaunchKernelGGL(k_permute_transpose, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, out, in, ta, batch);
+    KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes, true);
+    hipExtLaunchKernelGGL(k_permute_transpose, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0, out,
+                          in, ta, batch);
     check_launch("k_permute_transpose");
 }
 

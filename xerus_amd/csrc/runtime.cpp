@@ -67,8 +67,8 @@ void Pool::trim() {
     free_.clear();
 }
 
-KernelTimer::KernelTimer(xrs_handle_t h, uint32_t family, double flops, double bytes)
-    : h_(h), on_((h->prof_mask & family) != 0) {
+KernelTimer::KernelTimer(xrs_handle_t h, uint32_t family, double flops, double bytes, bool dispatch)
+    : h_(h), on_((h->prof_mask & family) != 0), dispatch_(dispatch) {
     if (!on_) return;
     auto get = [&]() {
         hipEvent_t e;
@@ -84,12 +84,12 @@ KernelTimer::KernelTimer(xrs_handle_t h, uint32_t family, double flops, double b
     rec_.stop = get();
     rec_.flops = flops;
     rec_.bytes = bytes;
-    XRS_HIP(hipEventRecord(rec_.start, h_->stream));
+    if (!dispatch_) XRS_HIP(hipEventRecord(rec_.start, h_->stream));
 }
 
 KernelTimer::~KernelTimer() {
     if (!on_) return;
-    (void)hipEventRecord(rec_.stop, h_->stream);
+    if (!dispatch_) (void)hipEventRecord(rec_.stop, h_->stream);
     h_->prof.push_back(rec_);
 }
 

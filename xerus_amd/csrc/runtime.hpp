@@ -151,12 +151,17 @@ struct DevBuf {
 // Kernel-duration instrumentation (xrs_prof_begin/end).
 class KernelTimer {
    public:
-    KernelTimer(xrs_handle_t h, uint32_t family, double flops, double bytes);
+    // dispatch = true: the caller launches with hipExtLaunchKernelGGL(..., start(), stop(), 0, ...), so the
+    // events carry the dispatch's own begin / end timestamps (the kernel-trace duration a profiler reports)
+    // instead of marker packets around it (which add the dispatch latency: ~6 us per TT-shape GEMM)
+    KernelTimer(xrs_handle_t h, uint32_t family, double flops, double bytes, bool dispatch = false);
     ~KernelTimer();
+    hipEvent_t start() const { return on_ ? rec_.start : nullptr; }
+    hipEvent_t stop() const { return on_ ? rec_.stop : nullptr; }
 
    private:
     xrs_handle_t h_;
-    bool on_;
+    bool on_, dispatch_;
     ProfRecord rec_{};
 };
 

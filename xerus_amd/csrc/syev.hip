@@ -353,80 +353,98 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
         // (no early exit for tau = 0: p = w = 0 then and the update leaves every entry unchanged; a second
         // loop latch would double the live matrix registers at the merge)
         const double tj = sh_tau;
-        // symmetric product: row sums of the stored entries, column sums of the strictly lower ones
-        double rp[NR];
+        // symmetric product and update from block row IA0 on: rows and columns <= j are finished (v and p
+        // vanish there, the update leaves them unchanged), so block rows ia < IA0 = (j + 1) / 32 and column
+        // blocks ib < 2 IA0 are skipped -- one compile-time loop nest per IA0 (a switch, no per-block
+        // branches). Their entries of psr / cbuf are not written; ps is 0 at indices <= j regardless.
+        auto step_from = [&](auto ia0_c) {
+            constexpr int IA0 = decltype(ia0_c)::value;
+            // symmetric product: row sums of the stored entries, column sums of the strictly lower ones
+            double rp[NR];
 #pragma unroll
-        for (int ia = 0; ia < NR; ++ia) rp[ia] = 0.0;
+            for (int ia = IA0; ia < NR; ++ia) rp[ia] = 0.0;
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-            double cp[8], vk[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                cp[q] = 0.0;
-                vk[q] = vs[tc + 16 * (8 * hh + q)];
-            }
-#pragma unroll
-            for (int ia = 0; ia < NR; ++ia) {
-                __builtin_amdgcn_sched_barrier(0);
-                const double vi = vs[tr + 32 * ia];
+            for (int hh = 0; hh < 2; ++hh) {
+                if (8 * hh + 7 < 2 * IA0) continue;   // (compile time) the whole half is finished
+                double cp[8], vk[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    const int ib = 8 * hh + q;
-                    if (ib <= 2 * ia + 1) {
-                        const double av = a[ia * (ia + 1) + ib];
-                        rp[ia] = fma(av, vk[q], rp[ia]);
-                        if (ib < 2 * ia) cp[q] = fma(av, vi, cp[q]);
-                        else cp[q] = fma((ib == 2 * ia ? low0 : low1) ? av : 0.0, vi, cp[q]);
+                    cp[q] = 0.0;
+                    vk[q] = vs[tc + 16 * (8 * hh + q)];
+                }
+#pragma unroll
+                for (int ia = IA0; ia < NR; ++ia) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const double vi = vs[tr + 32 * ia];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int ib = 8 * hh + q;
+                        if (ib >= 2 * IA0 && ib <= 2 * ia + 1) {
+                            const double av = a[ia * (ia + 1) + ib];
+                            rp[ia] = fma(av, vk[q], rp[ia]);
+                            if (ib < 2 * ia) cp[q] = fma(av, vi, cp[q]);
+                            else cp[q] = fma((ib == 2 * ia ? low0 : low1) ? av : 0.0, vi, cp[q]);
+                        }
                     }
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    if (8 * hh + q < 2 * IA0) continue;
+                    cp[q] += xor16(cp[q]);
+                    cp[q] += xor32(cp[q]);
+                }
+                if (lane < 16) {
+#pragma unroll
+                    for (int q = 0; q < 8; ++q)
+                        if (8 * hh + q >= 2 * IA0) cbuf[wave][tc + 16 * (8 * hh + q)] = cp[q];
                 }
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                cp[q] += xor16(cp[q]);
-                cp[q] += xor32(cp[q]);
+            for (int ia = IA0; ia < NR; ++ia) {
+                const double r = sum16(rp[ia]);
+                if (tc == 0) psr[tr + 32 * ia] = r;
             }
-            if (lane < 16) {
+            lds_barrier();
+            if (t < SY_MAX) {
+                double c = 0.0;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) cbuf[wave][tc + 16 * (8 * hh + q)] = cp[q];
+                for (int w = 0; w < NW; ++w) c += cbuf[w][t];
+                ps[t] = (t > j && t < n) ? tj * (psr[t] + c) : 0.0;
             }
-        }
+            lds_barrier();
+            // K = -(tau / 2) (p . v) in every wave, w = p + K v on the fly; A -= v w^T + w v^T on the kept entries
+            double sk = 0.0;
 #pragma unroll
-        for (int ia = 0; ia < NR; ++ia) {
-            const double r = sum16(rp[ia]);
-            if (tc == 0) psr[tr + 32 * ia] = r;
-        }
-        lds_barrier();
-        if (t < SY_MAX) {
-            double c = 0.0;
-#pragma unroll
-            for (int w = 0; w < NW; ++w) c += cbuf[w][t];
-            ps[t] = (t > j && t < n) ? tj * (psr[t] + c) : 0.0;
-        }
-        lds_barrier();
-        // K = -(tau / 2) (p . v) in every wave, w = p + K v on the fly; A -= v w^T + w v^T on the kept entries
-        double sk = 0.0;
-#pragma unroll
-        for (int q = 0; q < NP / 64; ++q) sk = fma(ps[lane + 64 * q], vs[lane + 64 * q], sk);
-        const double K = -0.5 * tj * sum64(sk);
-        {
+            for (int q = 0; q < NP / 64; ++q) sk = fma(ps[lane + 64 * q], vs[lane + 64 * q], sk);
+            const double K = -0.5 * tj * sum64(sk);
             double vi[NR], wi[NR];
 #pragma unroll
-            for (int ia = 0; ia < NR; ++ia) {
+            for (int ia = IA0; ia < NR; ++ia) {
                 vi[ia] = vs[tr + 32 * ia];
                 wi[ia] = fma(K, vi[ia], ps[tr + 32 * ia]);
             }
 #pragma unroll
-            for (int ib = 0; ib < 16; ++ib) {
+            for (int ib = 2 * IA0; ib < 16; ++ib) {
                 __builtin_amdgcn_sched_barrier(0);   // one column block at a time (hoisted operands spill)
                 const double vk = vs[tc + 16 * ib];
                 const double wk = fma(K, vk, ps[tc + 16 * ib]);
 #pragma unroll
-                for (int ia = ib / 2; ia < NR; ++ia) {
+                for (int ia = (ib / 2 > IA0 ? ib / 2 : IA0); ia < NR; ++ia) {
                     const int ix = ia * (ia + 1) + ib;
                     const double u = fma(-vi[ia], wk, fma(-wi[ia], vk, a[ix]));
                     a[ix] = (ib < 2 * ia || (ib == 2 * ia ? keep0 : keep1)) ? u : 0.0;
                 }
             }
+        };
+        switch ((j + 1) >> 5) {
+            case 0: step_from(std::integral_constant<int, 0>{}); break;
+            case 1: step_from(std::integral_constant<int, 1>{}); break;
+            case 2: step_from(std::integral_constant<int, 2>{}); break;
+            case 3: step_from(std::integral_constant<int, 3>{}); break;
+            case 4: step_from(std::integral_constant<int, 4>{}); break;
+            case 5: step_from(std::integral_constant<int, 5>{}); break;
+            case 6: step_from(std::integral_constant<int, 6>{}); break;
+            default: step_from(std::integral_constant<int, 7>{}); break;
         }
         L512_PUBLISH(j + 1);
     }

@@ -517,6 +517,28 @@ __global__ void k_add_identity(double* __restrict__ X, int n, double v) {
     if (i < n) X[size_t(i) * n + i] += v;
 }
 
+// Tall edges of the general round: after the cut of edge k + 1 the columns (i, b) of core_k with b >= the
+// device rank *kk (the padded ones) are exactly zero, so the Gram X^T X has exactly zero rows / columns
+// there. fill: those diagonal entries become the largest diagonal entry (the Cholesky factors the two
+// blocks independently and Q keeps zero columns there); fill = false: the final factor's padded diagonal
+// back to zero (R's padded rows / columns are then exactly zero: singular values 0, cut by the rank rule).
+__global__ void __launch_bounds__(256) k_pad_diag(double* __restrict__ G, int N, int b, const int* __restrict__ kk, bool fill) {
+    __shared__ double red[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int keep = *kk;
+    double v = 0.0;
+    if (fill) {
+        for (int p = t; p < N; p += 256) v = fmax(v, G[size_t(p) * N + p]);
+        for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+        if (lane == 0) red[w] = v;
+        __syncthreads();
+        v = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+        if (!(v > 0.0)) v = 1.0;
+    }
+    for (int p = t; p < N; p += 256)
+        if (p % b >= keep) G[size_t(p) * N + p] = v;
+}
+
 // flag = 1 unless 1 / ||W||_F > c ||X||_F with ||X||_F^2 = trace(G) (G: n x n Gram of the unfolding)
 __global__ void __launch_bounds__(256) k_rank_cert_gram(const double* __restrict__ W, const double* __restrict__ G, int n, double c,
                                                         int* __restrict__ flag) {
@@ -545,8 +567,10 @@ unsigned grid_for(size_t elems) { return unsigned(std::min<size_t>(std::max<size
 // Shifted CholeskyQR3, enqueued: tall A (m x n, m >= n) = Q R (RL = R, upper, n x n), or wide A (m x n,
 // m <= n) = L Q (RL = L, lower, m x m). st[0..3) potrf statuses; trG[0] = ||A||_F^2; with Rinv, the
 // explicit inverse of the triangular factor (tall: R^{-1} transposed, i.e. L3^{-1} L2^{-1} L1^{-1} --
-// same Frobenius norm). N = min(m, n) <= 512.
-void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL, int* st, double* trG, double* Rinv) {
+// same Frobenius norm). N = min(m, n) <= 512. pad_kk (tall only): the columns p with p % pad_b >= *pad_kk are
+// known to be zero (k_pad_diag).
+void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL, int* st, double* trG, double* Rinv,
+           const int* pad_kk = nullptr, int pad_b = 1) {
     xrs_handle_t h = sw.t.h;
     const size_t N = wide ? m : n, M = wide ? n : m;
     const int Ni = int(N);
@@ -562,6 +586,10 @@ void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q,
     for (int p = 0; p < 3; ++p) {
         if (wide) gemm_sym(h, L[p], N, 1.0, cur, n, false, M, cur, n, true);   // X X^T
         else gemm_sym(h, L[p], N, 1.0, cur, n, true, M, cur, n, false);        // X^T X
+        if (pad_kk && !wide) {
+            hipLaunchKernelGGL(k_pad_diag, dim3(1), dim3(256), 0, h->stream, L[p], Ni, pad_b, pad_kk, true);
+            check_launch("k_pad_diag");
+        }
         potrf(h, L[p], Ni, p == 0 ? s_rel : 0.0, Dv[p], st + p, p == 0 ? info : nullptr);
         trsm(h, wide, L[p], Dv[p], Ni, cur, n, outs[p], n, int(M));           // tall: X L^{-T}, wide: L^{-1} X
         cur = outs[p];
@@ -574,6 +602,10 @@ void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q,
     } else {
         gemm(h, G, N, N, 1.0, L[2], N, true, N, L[1], N, true);
         gemm(h, RL, N, N, 1.0, G, N, false, N, L[0], N, true);
+        if (pad_kk) {
+            hipLaunchKernelGGL(k_pad_diag, dim3(1), dim3(256), 0, h->stream, RL, Ni, pad_b, pad_kk, false);
+            check_launch("k_pad_diag");
+        }
     }
     if (Rinv) {   // L3^{-1} L2^{-1} L1^{-1} from the identity by three column TRSMs
         double* I0 = sw.buf(N * N);
@@ -720,7 +752,9 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         double* B = A[k];
         double* Qf = sw.buf(r * N);
         double* F = sw.buf(gg * gg);
-        scqr3(sw, B, r, N, wide, Qf, F, st + nst, nullptr, nullptr);
+        // (tall edge after a cut of edge k + 1: its padded zero columns, k_pad_diag)
+        const int* pad = (!wide && k + 1 < d) ? st + kRank + int(k + 1) : nullptr;
+        scqr3(sw, B, r, N, wide, Qf, F, st + nst, nullptr, nullptr, pad, int(g[k + 1]));
         nst += 3;
         double* S = sw.buf(gg);
         double* V = sw.buf(gg * gg);
