@@ -78,10 +78,11 @@ def random_cores(xe, dims, ranks, seed):
 
 def load_traffic():
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC pass of this bench (or None)."""
-    p = os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json")
-    if not os.path.exists(p):
-        p = os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json")
-    if not os.path.exists(p):
+    for tag in ("r04", "r03", "r02"):   # the newest committed pass
+        p = os.path.join(ROOT, "profiles", tag, "pmc_traffic.json")
+        if os.path.exists(p):
+            break
+    else:
         return None
     try:
         with open(p) as f:

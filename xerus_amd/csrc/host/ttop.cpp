@@ -27,6 +27,7 @@ size_t half(const std::vector<size_t>& _dims) { return _dims.size() / 2; }
 
 // the positions where an index list splits into two halves of `_half` modes each, or npos
 size_t split_point(const std::vector<Index>& _idx, size_t _degree) {
+    if (_degree == 0) return _idx.size() % 2 == 0 ? _idx.size() / 2 : std::string::npos;   // A(i/2, j/2) of order 0
     size_t span = 0, k = 0;
     while (k < _idx.size() && span < _degree / 2) span += _idx[k++].actual_span(_degree);
     return span == _degree / 2 ? k : std::string::npos;
@@ -424,6 +425,13 @@ TTTensor IndexedTTStack::evaluate_tt() const {
     std::vector<size_t> n(op->dimensions.begin(), op->dimensions.begin() + long(d));
     std::vector<size_t> m(op->dimensions.begin() + long(d), op->dimensions.end());
     XERUS_REQUIRE(std::vector<size_t>(vec->dimensions) == (transposed ? n : m), "TTOperator * TTTensor: mode sizes differ");
+    if (d == 0) {   // order 0: the product of the two scalars
+        TTTensor result(std::vector<size_t>{});
+        Tensor c = op->components[0];
+        c *= vec->components[0][size_t(0)];
+        result.components[0] = std::move(c);
+        return result;
+    }
     const CoreView A = view_op(*op), X = view_tt(*vec);
     std::vector<double*> out(d, nullptr);
     guard([&] {
@@ -451,6 +459,13 @@ TTOperator IndexedTTStack::evaluate_op() const {
     std::vector<size_t> mb(rhsOp->dimensions.begin(), rhsOp->dimensions.begin() + long(d));
     std::vector<size_t> p(rhsOp->dimensions.begin() + long(d), rhsOp->dimensions.end());
     XERUS_REQUIRE(m == mb, "TTOperator * TTOperator: mode sizes differ");
+    if (d == 0) {
+        TTOperator result(std::vector<size_t>{});
+        Tensor c = op->components[0];
+        c *= rhsOp->components[0][size_t(0)];
+        result.components[0] = std::move(c);
+        return result;
+    }
     const CoreView A = view_op(*op), B = view_op(*rhsOp);
     std::vector<double*> out(d, nullptr);
     guard([&] {

@@ -621,6 +621,9 @@ void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q,
 
 }  // namespace
 
+// xerus::EPSILON, the default eps of round(maxRanks): an eps above it may cut an edge arbitrarily deep
+constexpr double kDefaultEps = 8 * 2.220446049250313e-16;
+
 bool round_general(TT& t, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
@@ -745,7 +748,28 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
     // 2. right to left, uncut (padded) sizes: g[k] = working rank of edge k
     std::vector<size_t> g(rr);
     std::vector<int> jac;
+    int nsync = 0;
     for (size_t k = d - 1; k >= 1; --k) {
+        // After the cut of edge k + 1 to its device rank kk, core_k keeps n_k (g_{k+1} - kk) zero columns. If
+        // r_k > n_k kk, its unfolding has rank < r_k: a wide Gram B B^T would be exactly singular (tall ones
+        // are masked, k_pad_diag). When the cut can go that deep (an eps cut, or maxRank n_k < r_k), read kk
+        // (one synchronisation) and compact core_k to its kk right columns; core_{k+1}'s first kk rows
+        // already hold the kept rows.
+        if (k + 1 < d && g[k] > t.n[k] && (eps > kDefaultEps || max_ranks[k] * t.n[k] < g[k])) {
+            int* kh = hs + kSlots - 1;
+            XRS_HIP(hipMemcpyAsync(kh, st + kRank + int(k + 1), 4, hipMemcpyDeviceToHost, h->stream));
+            host_wait(h);
+            ++nsync;
+            const size_t v = size_t(*kh);
+            if (*kh >= 1 && v < g[k + 1] && v * t.n[k] < g[k]) {
+                const size_t rows = g[k] * t.n[k], gb = g[k + 1];
+                double* Cc = sw.core(rows * v);
+                XRS_HIP(hipMemcpy2DAsync(Cc, v * 8, A[k], gb * 8, v * 8, rows, hipMemcpyDeviceToDevice, h->stream));
+                sw.drop(A[k]);
+                A[k] = Cc;
+                g[k + 1] = v;
+            }
+        }
         const size_t r = g[k], N = t.n[k] * g[k + 1];
         const bool wide = r <= N;
         const size_t gg = wide ? r : N;
@@ -810,8 +834,8 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         kk[k] = size_t(std::max(v, 1));
     }
     if (dbg) {
-        std::fprintf(stderr, "round_general: %s (first failing status slot %d), max Jacobi sweeps %d; per edge:", ok ? "certified" : "NOT certified",
-                     bad, max_sweeps);
+        std::fprintf(stderr, "round_general: %s (first failing status slot %d), max Jacobi sweeps %d, %d rank read-backs; per edge:",
+                     ok ? "certified" : "NOT certified", bad, max_sweeps, nsync);
         for (size_t i = 0; i < jac.size(); ++i) std::fprintf(stderr, " %d:%d", jac[i], hs[kJac + int(i)]);
         std::fprintf(stderr, "\n");
     }
