@@ -16,6 +16,8 @@ PERMS = [
     ((3, 5, 7, 11), (2, 0, 3, 1)),
     ((2, 3, 4, 5, 6), (4, 2, 0, 1, 3)),
     ((33, 65), (1, 0)),                   # ragged tiles
+    ((3, 128, 192), (0, 2, 1)),           # 64 x 64 16-B tiles, batched
+    ((192, 5, 64), (2, 1, 0)),            # 64 x 64 tiles with an odd batch stride (16-B path off)
     ((1, 7, 1), (2, 1, 0)),
     ((5,), (0,)),
     ((0, 4), (1, 0)),                     # empty

@@ -7,6 +7,7 @@
 //   (b) a batched 2-D transpose between the input-contiguous mode `a` and the output-contiguous
 //       mode `b`: 32x32 fp64 tiles staged through LDS ([32][33] padding: conflict-free ds_read_b64
 //       columns), coalesced 256-B row segments on both the HBM read and the HBM write; or
+//       64x64 tiles with 16-B accesses when both modes span whole tiles and everything is 16-B aligned;
 //   (c) when those modes are shorter than a tile, the same transpose between GROUPS of innermost
 //       input / output modes (flattened indices), so small modes still fill whole tiles.
 // Both are HBM-bound: algorithmic bytes = 2 * size * 8.
@@ -163,6 +164,50 @@ __global__ void __launch_bounds__(256) k_permute_transpose(double* __restrict__ 
         for (int j = 0; j < TT; j += 8) {
             const size_t ia = a0 + ty + j, ib = b0 + tx;
             if (ib < a.db && ia < a.da) out[ooff + ia * a.out_sa + ib] = tile[tx][ty + j];
+        }
+        __syncthreads();
+    }
+}
+
+// (b') the same batched transpose with 64 x 64 tiles and 16-B accesses, for aligned operands whose two
+// modes span whole tiles (da, db % 64 == 0, even strides and offsets): a wave moves 1 KB per instruction
+// (two 512-B row segments), each thread keeps 8 loads in flight (32 KB per workgroup per round trip)
+// instead of 4 x 8 B -- the mid-size transposes (16-21 MB) are bound by that round trip, not by HBM.
+// LDS rows of 65 doubles: the column reads of ds_read_b64 (row stride 130 banks) hit distinct bank pairs.
+constexpr int TW = 64;
+typedef double dv2 __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256) k_permute_transpose64(double* __restrict__ out, const double* __restrict__ in, TrArgs a,
+                                                             size_t batch) {
+    __shared__ double tile[TW][TW + 1];
+    const unsigned t = blockIdx.x;
+    const size_t a0 = size_t(t % a.tiles_a) * TW, b0 = size_t(t / a.tiles_a) * TW;
+    const int tx = threadIdx.x & 31;   // double2 column within a 64-wide row
+    const int ty = threadIdx.x >> 5;   // 0..7
+    for (size_t bi = blockIdx.y; bi < batch; bi += gridDim.y) {
+        unsigned rem = unsigned(bi);
+        size_t ioff = 0, ooff = 0;
+        for (int k = a.nb - 1; k >= 0; --k) {
+            const unsigned dk = unsigned(a.bdims[k]), q = rem / dk, i = rem - q * dk;
+            rem = q;
+            ioff += size_t(i) * a.bin_str[k];
+            ooff += size_t(i) * a.bout_str[k];
+        }
+        dv2 v[TW / 8];
+#pragma unroll
+        for (int j = 0; j < TW / 8; ++j)   // input rows along b, 16 B per lane along a
+            v[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(in + ioff + (b0 + ty + 8 * j) * a.in_sb + a0) + tx);
+#pragma unroll
+        for (int j = 0; j < TW / 8; ++j) {
+            tile[ty + 8 * j][2 * tx] = v[j].x;
+            tile[ty + 8 * j][2 * tx + 1] = v[j].y;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < TW / 8; ++j) {   // output rows along a, 16 B per lane along b
+            dv2 w;
+            w.x = tile[2 * tx][ty + 8 * j];
+            w.y = tile[2 * tx + 1][ty + 8 * j];
+            __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(out + ooff + (a0 + ty + 8 * j) * a.out_sa + b0) + tx);
         }
         __syncthreads();
     }
@@ -334,11 +379,23 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
         ++ta.nb;
         batch *= p.dims[k];
     }
-    ta.tiles_a = unsigned((ta.da + TT - 1) / TT);
-    ta.tiles_b = unsigned((ta.db + TT - 1) / TT);
+    // 64 x 64 tiles with 16-B accesses when every row segment is a whole, 16-B aligned tile row
+    bool wide = ta.da % TW == 0 && ta.db % TW == 0 && ta.in_sb % 2 == 0 && ta.out_sa % 2 == 0 &&
+                ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+    for (int k = 0; k < ta.nb; ++k) wide = wide && ta.bin_str[k] % 2 == 0 && ta.bout_str[k] % 2 == 0;
+    const int tw = wide ? TW : TT;
+    ta.tiles_a = unsigned((ta.da + tw - 1) / tw);
+    ta.tiles_b = unsigned((ta.db + tw - 1) / tw);
     const size_t tiles = size_t(ta.tiles_a) * ta.tiles_b;
     XRS_REQUIRE(tiles < (1ull << 31) && batch < (1ull << 32), "permutation too large");
     const unsigned gy = unsigned(std::min<size_t>(batch, 65535));
+    if (wide) {
+        KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes, true);
+        hipExtLaunchKernelGGL(k_permute_transpose64, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0,
+                              out, in, ta, batch);
+        check_launch("k_permute_transpose64");
+        return;
+    }
     KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes, true);
     hipExtLaunchKernelGGL(k_permute_transpose, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0, out,
                           in, ta, batch);
