@@ -4,10 +4,11 @@
 // (tt_trunc.hip round_truncate), the kept left singular vectors of B are the eigenvectors of P's kk
 // largest eigenvalues. Three launches, LAPACK's dsytrd / dstebz / dstein / dormtr structure:
 //   1. k_sytrd: Householder tridiagonalisation A = Q T Q^T in ONE workgroup, the matrix register-resident
-//      (n <= 128: 1024 threads on a 32 x 32 grid, element (i, k) on thread (i mod 32, k mod 32): the
-//      shrinking trailing block stays spread over every thread; 129..256: k_sytrd_l512, 512 threads holding
-//      the lower block triangle). Per column: the reflector from one wave, the symmetric matrix-vector
-//      product with in-wave DPP / permlane reductions, the rank-2 update in registers -- LDS-only barriers.
+//      (n <= 64: 1024 threads on a 32 x 32 grid, element (i, k) on thread (i mod 32, k mod 32): the
+//      shrinking trailing block stays spread over every thread; 65..256: k_sytrd_l512<NR>, 512 threads
+//      holding the lower block triangle of NR 32-row block rows, finished block rows / columns skipped by a
+//      compile-time switch). Per column: the reflector from one wave, the symmetric matrix-vector product
+//      with in-wave DPP / permlane reductions, the rank-2 update in registers -- LDS-only barriers.
 //   2. k_stebz_stein: one wave per wanted eigenvalue (kk workgroups in parallel): Sturm-count
 //      multisection on 64 points per round (~9 rounds to full precision), then inverse iteration with the
 //      partially pivoted LU of T - lambda I (dgttrf / dgttrs), three solves from a fixed start vector.
@@ -269,9 +270,10 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
 // row) plus, for the mirrored upper triangle, the columns of the strictly lower ones (over the 4 rows of a
 // wave by permlane16 / shuffle, then over the 8 waves through LDS). The column halves (ib < 8, ib >= 8) are
 // processed one after the other to bound the live operand registers.
+template <int NR>   // 32-row block rows: 8 (orders <= 256) or 4 (orders <= 128)
 __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
                                                    double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V) {
-    constexpr int NR = 8, NW = 8, NP = 256;
+    constexpr int NW = 8, NP = 32 * NR;
     constexpr int NL = NR * (NR + 1);   // block row ia holds column blocks 0 .. 2 ia + 1: offset ia (ia + 1)
     __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX], psr[SY_MAX], cbuf[NW][SY_MAX];
     __shared__ double sh_tau;
@@ -365,7 +367,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
             for (int ia = IA0; ia < NR; ++ia) rp[ia] = 0.0;
 #pragma unroll
             for (int hh = 0; hh < 2; ++hh) {
-                if (8 * hh + 7 < 2 * IA0) continue;   // (compile time) the whole half is finished
+                if (8 * hh + 7 < 2 * IA0 || 8 * hh >= 2 * NR) continue;   // (compile time) finished / absent half
                 double cp[8], vk[8];
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
@@ -424,7 +426,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                 wi[ia] = fma(K, vi[ia], ps[tr + 32 * ia]);
             }
 #pragma unroll
-            for (int ib = 2 * IA0; ib < 16; ++ib) {
+            for (int ib = 2 * IA0; ib < 2 * NR; ++ib) {
                 __builtin_amdgcn_sched_barrier(0);   // one column block at a time (hoisted operands spill)
                 const double vk = vs[tc + 16 * ib];
                 const double wk = fma(K, vk, ps[tc + 16 * ib]);
@@ -440,11 +442,11 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
             case 0: step_from(std::integral_constant<int, 0>{}); break;
             case 1: step_from(std::integral_constant<int, 1>{}); break;
             case 2: step_from(std::integral_constant<int, 2>{}); break;
-            case 3: step_from(std::integral_constant<int, 3>{}); break;
-            case 4: step_from(std::integral_constant<int, 4>{}); break;
-            case 5: step_from(std::integral_constant<int, 5>{}); break;
-            case 6: step_from(std::integral_constant<int, 6>{}); break;
-            default: step_from(std::integral_constant<int, 7>{}); break;
+            case 3: step_from(std::integral_constant<int, (NR > 3 ? 3 : NR - 1)>{}); break;
+            case 4: step_from(std::integral_constant<int, (NR > 4 ? 4 : NR - 1)>{}); break;
+            case 5: step_from(std::integral_constant<int, (NR > 5 ? 5 : NR - 1)>{}); break;
+            case 6: step_from(std::integral_constant<int, (NR > 6 ? 6 : NR - 1)>{}); break;
+            default: step_from(std::integral_constant<int, NR - 1>{}); break;
         }
         L512_PUBLISH(j + 1);
     }
@@ -739,8 +741,8 @@ void sym_tridiag(xrs_handle_t h, const double* A, int lda, int n, double* d, dou
     XRS_REQUIRE(n >= 2 && n <= SY_MAX, "sym_tridiag: need 2 <= n <= 256");
     DevBuf tbuf(h, size_t(n) * 8), V(h, size_t(n) * n * 8);
     if (n <= 64) hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
-    else if (n <= 128) hipLaunchKernelGGL((k_sytrd<32, 4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
-    else hipLaunchKernelGGL(k_sytrd_l512, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d());
+    else if (n <= 128) hipLaunchKernelGGL(k_sytrd_l512<4>, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d());
+    else hipLaunchKernelGGL(k_sytrd_l512<8>, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d());
     check_launch("k_sytrd");
 }
 
@@ -753,15 +755,16 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     DevBuf sb(h, want_stamps ? 768 * 8 : 0);
     unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
     if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 768 * 8, h->stream));
-    // the 1024-thread grid up to 128 (measured faster than 256 threads with 64 elements each: 5.1 vs 5.6 ms
-    // per cfg3 round(64), profiles/r03/sytrd_grid_ab_r03q.txt -- one wave per SIMD is issue-bound in the
-    // update), the 512-thread lower-block grid above
+    // the 1024-thread grid up to 64 (r04 A/B, profiles/r04/sytrd_l512_ab_r04t.txt: order-64 edges 2.20 vs
+    // 2.38 ms per cfg3-shaped round(32) with the 512-thread kernel), the 512-thread lower-block grid with
+    // finished-block skipping above (order 128: 4.11 vs 4.58 ms per cfg3 round(64) against the 1024-thread
+    // grid; r03: the 1024-thread grid beat 256 threads with 64 elements each, 5.1 vs 5.6 ms)
     if (n <= 64) {
         hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
     } else if (n <= 128) {
-        hipLaunchKernelGGL((k_sytrd<32, 4>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
+        hipLaunchKernelGGL(k_sytrd_l512<4>, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
     } else {
-        hipLaunchKernelGGL(k_sytrd_l512, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
+        hipLaunchKernelGGL(k_sytrd_l512<8>, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
     }
     check_launch("k_sytrd");
     // the chains' reciprocals: 2 Newton steps after the hardware estimate (one step measured 4.40 vs 4.47 ms
