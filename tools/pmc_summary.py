@@ -69,8 +69,9 @@ if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
         "write_size_raw_kib": g["WRITE_SIZE"]["mean"],
         "calibration": {"fetch_factor": ff, "write_factor": wf, "measured": cal.get("factors", {})},
         "dispatches": g["FETCH_SIZE"]["dispatches"],
-        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over bench.py --no-cpu --no-cfg5 --no-extras "
-                  "--steps 3 --warmup 1, mean per GEMM dispatch (k_gemm_glds + k_gemm_f64), corrected by the 8-B load/store calibration of "
+        "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over " + os.environ.get(
+                      "PMC_CMD", "python3 bench.py --no-cpu --no-cfg5 --no-extras --no-overlap --steps 20 --warmup 3 (tools/gpu_run.sh pmc)") +
+                  ", mean per GEMM dispatch (k_gemm_glds + k_gemm_f64), corrected by the 8-B load/store calibration of "
                   "tools/fetch_calib.hip (FETCH x%.3f, WRITE x%.3f); %s/pmc_summary.json" % (ff, wf, dst),
     }
     if "SQ_VALU_MFMA_BUSY_CYCLES" in g and "GRBM_GUI_ACTIVE" in g:
