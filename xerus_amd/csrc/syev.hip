@@ -474,8 +474,13 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 // did not reach full precision.
 template <int NEWTON>
 __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
-                                                     double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status) {
-    __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX];
+                                                     double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status,
+                                                     unsigned long long* __restrict__ stamps) {
+    // diagnostics (stamps != null): workgroup 0 records s_memtime at its phase boundaries
+#define STEIN_STAMP(p) \
+    do { if (stamps && blockIdx.x == 0 && threadIdx.x == 0) stamps[p] = __builtin_amdgcn_s_memtime(); } while (0)
+    STEIN_STAMP(0);
+    __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX], sds[SY_MAX], se2s[SY_MAX];
     __shared__ double ld[SY_MAX], ldl[SY_MAX], ldu[SY_MAX], ldu2[SY_MAX], lb[SY_MAX];
     __shared__ int lpiv[SY_MAX];
     const int lane = threadIdx.x, q = blockIdx.x, m = n - 1 - q;
@@ -498,7 +503,15 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         emax2 = fmax(emax2, __shfl_xor(emax2, o, 64));
         amax = fmax(amax, __shfl_xor(amax, o, 64));
     }
+    // the multisection's three-term recurrence runs on T scaled by a power of two (exact: the counts are
+    // those of T) so that |d - x| and e^2 stay O(1) and 4 levels cannot overflow between rescalings
+    const double tsc = ldexp(1.0, -ilogb(fmax(amax, 1e-300)));
+    for (int i = lane; i < n; i += 64) {
+        sds[i] = sd[i] * tsc;
+        se2s[i] = se2[i] * (tsc * tsc);
+    }
     __syncthreads();
+    STEIN_STAMP(1);
     const double pivmin = 1e-290 * fmax(1.0, emax2);
     const double span = fmax(gu - gl, 1e-300);
     double lo = gl - 2.2e-16 * span - pivmin, hi = gu + 2.2e-16 * span + pivmin;
@@ -507,13 +520,42 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     bool done = false;
     for (; rounds < 16 && !done; ++rounds) {
         const double x = lo + (hi - lo) * double(lane + 1) * (1.0 / 65.0);
-        double qv = sd[0] - x;
-        if (fabs(qv) < pivmin) qv = -pivmin;
-        int c = qv < 0.0;
-        for (int i = 1; i < n; ++i) {
-            qv = (sd[i] - x) - se2[i - 1] * rcpn<NEWTON>(qv);
-            if (fabs(qv) < pivmin) qv = -pivmin;
-            c += qv < 0.0;
+        // Sturm count as sign changes of the leading minors p_i = (d_i - x) p_{i-1} - e_{i-1}^2 p_{i-2}
+        // (the pivots q_i = p_i / p_{i-1} of the q-form without its division: one FMA per level on the
+        // dependent chain instead of a reciprocal, two Newton steps and an FMA; the count is off the chain).
+        // The q-form's |q_i| < pivmin -> -pivmin guards its next division; here a tiny p_i only makes the
+        // next minor -e^2 p_{i-1}, and an exact zero (x an eigenvalue of a leading block) counted as
+        // non-negative moves x to either end of the bracket, which still contains the eigenvalue.
+        // p_{i-1}, p_{i-2} are rescaled by a power of two every 4 levels (|p_i| grows at most 4x per level
+        // on the scaled T).
+        const double xs = x * tsc, pivs = pivmin * tsc;
+        double pm2 = 1.0, pm1 = sds[0] - xs;
+        if (fabs(pm1) < pivs) pm1 = -pivs;
+        int c = pm1 < 0.0;
+        int i = 1;
+        for (; i + 4 <= n; i += 4) {
+            double dx[4], e2[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                dx[u] = sds[i + u] - xs;
+                e2[u] = se2s[i + u - 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const double pv = fma(dx[u], pm1, -e2[u] * pm2);
+                c += (pv < 0.0) != (pm1 < 0.0);
+                pm2 = pm1;
+                pm1 = pv;
+            }
+            const int ex = __builtin_amdgcn_frexp_exp(pm1);
+            pm1 = ldexp(pm1, -ex);
+            pm2 = ldexp(pm2, -ex);
+        }
+        for (; i < n; ++i) {
+            const double pv = fma(sds[i] - xs, pm1, -se2s[i - 1] * pm2);
+            c += (pv < 0.0) != (pm1 < 0.0);
+            pm2 = pm1;
+            pm1 = pv;
         }
         double nlo = c <= m ? x : -1e300, nhi = c >= m + 1 ? x : 1e300;
 #pragma unroll
@@ -526,43 +568,59 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         // absolute accuracy u ||T|| (dstebz's default abstol): all a backward-stable reduction delivers
         done = (hi - lo) <= 2.2204460492503131e-16 * (2.0 * fmax(fabs(lo), fabs(hi)) + 4.0 * span) + 2.0 * pivmin;
     }
+    STEIN_STAMP(2);
     const double lmb = 0.5 * (lo + hi);
     __shared__ double ild[SY_MAX];   // inverse pivots of U
     if (lane == 0) {
         lam[q] = lmb;
         if (!done) atomicMin(status, -1);
         // inverse iteration: T - lambda I = P L U (dgttrf, row interchanges where the subdiagonal entry is
-        // larger), tiny pivots replaced by u ||T|| (dlagtf's perturbation)
-        for (int i = 0; i < n; ++i) {
-            ld[i] = sd[i] - lmb;
-            ldl[i] = i + 1 < n ? se[i] : 0.0;
-            ldu[i] = i + 1 < n ? se[i] : 0.0;
-            ldu2[i] = 0.0;
-            lpiv[i] = i;
-        }
-        for (int i = 0; i + 1 < n; ++i) {
-            if (fabs(ld[i]) >= fabs(ldl[i])) {
-                if (ld[i] != 0.0) {
-                    const double f = ldl[i] * rcpn<NEWTON>(ld[i]);
-                    ldl[i] = f;
-                    ld[i + 1] -= f * ldu[i];
-                }
-            } else {
-                const double f = ld[i] * rcpn<NEWTON>(ldl[i]);
-                ld[i] = ldl[i];
+        // larger), tiny pivots replaced by u ||T|| (dlagtf's perturbation). The running diagonal and
+        // superdiagonal entries are carried in registers (no LDS store -> load per level on the dependent
+        // chain); the original entries of the next row are independent of it.
+        double dcur = sd[0] - lmb, ucur = n > 1 ? se[0] : 0.0;
+        auto lu_level = [&](int i, double l, double dn, double un) {
+            if (fabs(dcur) >= fabs(l)) {
+                const double f = dcur != 0.0 ? l * rcpn<NEWTON>(dcur) : 0.0;
+                ld[i] = dcur;
                 ldl[i] = f;
-                const double tmp = ldu[i];
-                ldu[i] = ld[i + 1];
-                ld[i + 1] = tmp - f * ld[i + 1];
-                if (i + 2 < n) {
-                    ldu2[i] = ldu[i + 1];
-                    ldu[i + 1] = -f * ldu[i + 1];
-                }
+                ldu[i] = ucur;
+                ldu2[i] = 0.0;
+                lpiv[i] = i;
+                dcur = dn - f * ucur;
+                ucur = un;
+            } else {
+                const double f = dcur * rcpn<NEWTON>(l);
+                ld[i] = l;
+                ldl[i] = f;
+                ldu[i] = dn;
+                ldu2[i] = un;
                 lpiv[i] = i + 1;
+                dcur = ucur - f * dn;
+                ucur = -f * un;
             }
+        };
+        int i = 0;
+        for (; i + 9 < n; i += 8) {   // the block's original entries read ahead of its chain
+            double l8[8], d8[8], u8[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                l8[u] = se[i + u];
+                d8[u] = sd[i + u + 1] - lmb;
+                u8[u] = se[i + u + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) lu_level(i + u, l8[u], d8[u], u8[u]);
         }
+        for (; i + 1 < n; ++i) lu_level(i, se[i], sd[i + 1] - lmb, i + 2 < n ? se[i + 1] : 0.0);
+        ld[n - 1] = dcur;
+        ldl[n - 1] = 0.0;
+        ldu[n - 1] = 0.0;
+        ldu2[n - 1] = 0.0;
+        lpiv[n - 1] = n - 1;
     }
     __syncthreads();
+    STEIN_STAMP(3);
     {
         const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
         for (int i = lane; i < n; i += 64) {
@@ -573,10 +631,38 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         }
     }
     __syncthreads();
+    STEIN_STAMP(4);
     for (int it = 0; it < 3; ++it) {
-        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in registers)
+        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in
+                           // registers, each block's 8 levels of LU operands read ahead of its dependent chain)
+            // forward: cur' = a_i cur + b_i with (a, b) = (-f, nxt) (no interchange) or (1, -f nxt) (rows i,
+            // i+1 swapped) formed off the chain; backward: x_i = alpha_i x_{i+1} + (beta_i x_{i+2} + gamma_i)
+            // -- one FMA per level on each dependent chain
             double cur = lb[0];
-            for (int i = 0; i + 1 < n; ++i) {
+            int i = 0;
+            for (; i + 8 < n; i += 8) {
+                double nx[8], fl[8];
+                int pv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    nx[u] = lb[i + u + 1];
+                    fl[u] = ldl[i + u];
+                    pv[u] = lpiv[i + u];
+                }
+                double ca[8], cb[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bool sw = pv[u] != i + u;
+                    ca[u] = sw ? 1.0 : -fl[u];
+                    cb[u] = sw ? -fl[u] * nx[u] : nx[u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    lb[i + u] = (pv[u] != i + u) ? nx[u] : cur;
+                    cur = fma(ca[u], cur, cb[u]);
+                }
+            }
+            for (; i + 1 < n; ++i) {
                 const double nxt = lb[i + 1], f = ldl[i];
                 if (lpiv[i] == i) {
                     lb[i] = cur;
@@ -588,7 +674,25 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
             }
             double x1 = cur * ild[n - 1], x2 = 0.0;
             lb[n - 1] = x1;
-            for (int i = n - 2; i >= 0; --i) {
+            i = n - 2;
+            for (; i >= 7; i -= 8) {
+                double al[8], be[8], ga[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const double iv = ild[i - u];
+                    al[u] = -iv * ldu[i - u];
+                    be[u] = -iv * ldu2[i - u];
+                    ga[u] = iv * lb[i - u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const double x0 = fma(al[u], x1, fma(be[u], x2, ga[u]));
+                    lb[i - u] = x0;
+                    x2 = x1;
+                    x1 = x0;
+                }
+            }
+            for (; i >= 0; --i) {
                 const double x0 = (lb[i] - ldu[i] * x1 - ldu2[i] * x2) * ild[i];
                 lb[i] = x0;
                 x2 = x1;
@@ -596,6 +700,7 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
             }
         }
         __syncthreads();
+        STEIN_STAMP(5 + 2 * it);
         // normalise (scaled 2-norm over the wave)
         double mx = 0.0;
         for (int i = lane; i < n; i += 64) mx = fmax(mx, fabs(lb[i]));
@@ -612,8 +717,11 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         __syncthreads();
         for (int i = lane; i < n; i += 64) lb[i] *= sc;
         __syncthreads();
+        STEIN_STAMP(6 + 2 * it);
     }
     for (int i = lane; i < n; i += 64) Zt[size_t(q) * ldz + i] = lb[i];
+    STEIN_STAMP(11);
+#undef STEIN_STAMP
 }
 
 
@@ -752,9 +860,9 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     double* lm = lam ? lam : lbuf.d();
     KernelTimer timer(h, XRS_KFAM_SVD, 4.0 / 3.0 * double(n) * n * n + 4.0 * double(n) * n * kk, 8.0 * double(n) * n * 2);
     static const bool want_stamps = stamps_enabled("syev");
-    DevBuf sb(h, want_stamps ? 768 * 8 : 0);
+    DevBuf sb(h, want_stamps ? 1024 * 8 : 0);
     unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
-    if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 768 * 8, h->stream));
+    if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 1024 * 8, h->stream));
     // the 1024-thread grid up to 64 (r04 A/B, profiles/r04/sytrd_l512_ab_r04t.txt: order-64 edges 2.20 vs
     // 2.38 ms per cfg3-shaped round(32) with the 512-thread kernel), the 512-thread lower-block grid with
     // finished-block skipping above (order 128: 4.11 vs 4.58 ms per cfg3 round(64) against the 1024-thread
@@ -769,7 +877,8 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     check_launch("k_sytrd");
     // the chains' reciprocals: 2 Newton steps after the hardware estimate (one step measured 4.40 vs 4.47 ms
     // per cfg3 round(64) but multiplies the kept sigma's relative error by ~20)
-    hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status);
+    hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status,
+                       stp ? stp + 768 : nullptr);
     check_launch("k_stebz_stein");
     hipLaunchKernelGGL(k_cluster_orth, dim3(1), dim3(256), 0, h->stream, lm, dbuf.d(), ebuf.d(), n, kk, Ut, ldu);
     check_launch("k_cluster_orth");
@@ -777,6 +886,14 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     else if (n <= 128) hipLaunchKernelGGL((k_ormtr<2>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     else hipLaunchKernelGGL((k_ormtr<4>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     check_launch("k_ormtr");
+    if (stp) {   // k_stebz_stein phases of workgroup 0 (cycles)
+        std::vector<unsigned long long> hs(12);
+        XRS_HIP(hipMemcpyAsync(hs.data(), stp + 768, 12 * 8, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        std::fprintf(stderr, "k_stebz_stein n=%d: prologue %llu multisection %llu LU %llu pivots %llu solve/normalise %llu/%llu %llu/%llu %llu/%llu store %llu\n", n,
+                     hs[1] - hs[0], hs[2] - hs[1], hs[3] - hs[2], hs[4] - hs[3], hs[5] - hs[4], hs[6] - hs[5], hs[7] - hs[6],
+                     hs[8] - hs[7], hs[9] - hs[8], hs[10] - hs[9], hs[11] - hs[10]);
+    }
     if (stp) {   // per-phase cycles of the first steps: (b)-wait, reflector, wait, symv, wait, update (+ column)
         std::vector<unsigned long long> hst(768);
         XRS_HIP(hipMemcpyAsync(hst.data(), stp, 768 * 8, hipMemcpyDeviceToHost, h->stream));
