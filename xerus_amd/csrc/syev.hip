@@ -10,12 +10,14 @@
 //      compile-time switch). Per column: the reflector from one wave, the symmetric matrix-vector product
 //      with in-wave DPP / permlane reductions, the rank-2 update in registers -- LDS-only barriers.
 //   2. k_stebz_stein: one wave per wanted eigenvalue (kk workgroups in parallel): Sturm-count
-//      multisection on 64 points per round (~9 rounds to full precision), then inverse iteration with the
-//      partially pivoted LU of T - lambda I (dgttrf / dgttrs), three solves from a fixed start vector.
+//      multisection on 64 points per round (~9 rounds to full precision; the counts as sign changes of the
+//      three-term minor recurrence, one FMA per level on the chain), then inverse iteration with the
+//      partially pivoted LU of T - lambda I (dgttrf / dgttrs), three solves from a fixed start vector, every
+//      chain fed by operands read ahead in blocks (r04: 104 -> 73 us at order 128, the chains now
+//      FP64-issue-bound, profiles/r04/stein_phases_r04z.txt).
 //      Measured alternatives (profiles/r03/stein_variants_r03r.txt): a single twisted-factorisation solve
 //      (orthogonality only 1e-12..1e-11 on flat spectra, T - lambda I not being a relatively robust
-//      representation); 4 waves with 512 points per round and register-prefetched chains (6 instead of 9
-//      rounds, same 105 us: every O(n) chain is bound by its ~20-cycle dependent FP64 latency per level).
+//      representation); 4 waves with 512 points per round (6 instead of 9 rounds, no gain with r03's chains).
 //   3. k_ormtr: the eigenvectors back to A's coordinates, u = H_0 ... H_{n-2} z, one wave per vector
 //      (64 lanes, 4 vectors per workgroup), the reflectors staged through LDS in chunks.
 //   2b. k_cluster_orth: vectors of eigenvalue clusters (gaps <= 1e-3 ||T||, dstein's ORTOL) orthonormalised
