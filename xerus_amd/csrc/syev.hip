@@ -474,8 +474,9 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 // one 64-lane workgroup per wanted eigenvalue: block q -> the q-th largest (ascending index n - 1 - q).
 // Zt (kk x ldz): row q = the eigenvector of T (normalised); lam[q]. status[0] <- -1 if a multisection
 // did not reach full precision.
+constexpr int SW_WAVES = 4;   // waves of the multisection (k_stebz_stein)
 template <int NEWTON>
-__global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
+__global__ void __launch_bounds__(64 * SW_WAVES) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
                                                      double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status,
                                                      unsigned long long* __restrict__ stamps) {
     // diagnostics (stamps != null): workgroup 0 records s_memtime at its phase boundaries
@@ -485,7 +486,7 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     __shared__ double sd[SY_MAX], se[SY_MAX], se2[SY_MAX], sds[SY_MAX], se2s[SY_MAX];
     __shared__ double ld[SY_MAX], ldl[SY_MAX], ldu[SY_MAX], ldu2[SY_MAX], lb[SY_MAX];
     __shared__ int lpiv[SY_MAX];
-    const int lane = threadIdx.x, q = blockIdx.x, m = n - 1 - q;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = blockIdx.x, m = n - 1 - q;
     double gl = 1e300, gu = -1e300, emax2 = 0.0, amax = 0.0;
     for (int i = lane; i < n; i += 64) {
         const double di = d[i], ei = i + 1 < n ? e[i] : 0.0, em = i > 0 ? e[i - 1] : 0.0;
@@ -517,11 +518,13 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     const double pivmin = 1e-290 * fmax(1.0, emax2);
     const double span = fmax(gu - gl, 1e-300);
     double lo = gl - 2.2e-16 * span - pivmin, hi = gu + 2.2e-16 * span + pivmin;
-    // multisection: lane l counts the eigenvalues below lo + (hi - lo) (l + 1) / 65
+    // multisection: thread t counts the eigenvalues below lo + (hi - lo) (t + 1) / (64 SW_WAVES + 1); the
+    // waves (one per SIMD: the chains are FP64-issue-bound) merge their brackets through LDS every round
+    __shared__ double rlo[2][SW_WAVES], rhi[2][SW_WAVES];
     int rounds = 0;
     bool done = false;
     for (; rounds < 16 && !done; ++rounds) {
-        const double x = lo + (hi - lo) * double(lane + 1) * (1.0 / 65.0);
+        const double x = lo + (hi - lo) * double(tid + 1) * (1.0 / (64.0 * SW_WAVES + 1.0));
         // Sturm count as sign changes of the leading minors p_i = (d_i - x) p_{i-1} - e_{i-1}^2 p_{i-2}
         // (the pivots q_i = p_i / p_{i-1} of the q-form without its division: one FMA per level on the
         // dependent chain instead of a reciprocal, two Newton steps and an FMA; the count is off the chain).
@@ -565,6 +568,16 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
             nlo = fmax(nlo, __shfl_xor(nlo, o, 64));
             nhi = fmin(nhi, __shfl_xor(nhi, o, 64));
         }
+        if (lane == 0) {
+            rlo[rounds & 1][wave] = nlo;
+            rhi[rounds & 1][wave] = nhi;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < SW_WAVES; ++w) {
+            nlo = fmax(nlo, rlo[rounds & 1][w]);
+            nhi = fmin(nhi, rhi[rounds & 1][w]);
+        }
         if (nlo > lo) lo = nlo;
         if (nhi < hi) hi = nhi;
         // absolute accuracy u ||T|| (dstebz's default abstol): all a backward-stable reduction delivers
@@ -573,7 +586,7 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     STEIN_STAMP(2);
     const double lmb = 0.5 * (lo + hi);
     __shared__ double ild[SY_MAX];   // inverse pivots of U
-    if (lane == 0) {
+    if (tid == 0) {
         lam[q] = lmb;
         if (!done) atomicMin(status, -1);
         // inverse iteration: T - lambda I = P L U (dgttrf, row interchanges where the subdiagonal entry is
@@ -625,7 +638,7 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     STEIN_STAMP(3);
     {
         const double tiny = 2.2204460492503131e-16 * fmax(amax, 1e-300);
-        for (int i = lane; i < n; i += 64) {
+        for (int i = tid; i < n; i += 64 * SW_WAVES) {
             double p = ld[i];
             if (fabs(p) < tiny) p = copysign(tiny, p == 0.0 ? 1.0 : p);
             ild[i] = rcp2(p);
@@ -635,7 +648,7 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
     __syncthreads();
     STEIN_STAMP(4);
     for (int it = 0; it < 3; ++it) {
-        if (lane == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in
+        if (tid == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in
                            // registers, each block's 8 levels of LU operands read ahead of its dependent chain)
             // forward: cur' = a_i cur + b_i with (a, b) = (-f, nxt) (no interchange) or (1, -f nxt) (rows i,
             // i+1 swapped) formed off the chain; backward: x_i = alpha_i x_{i+1} + (beta_i x_{i+2} + gamma_i)
@@ -717,11 +730,12 @@ __global__ void __launch_bounds__(64) k_stebz_stein(const double* __restrict__ d
         ss = sum64(ss);
         const double sc = inv_mx / sqrt(ss);
         __syncthreads();
-        for (int i = lane; i < n; i += 64) lb[i] *= sc;
+        if (wave == 0)   // (every wave formed the same scale)
+            for (int i = lane; i < n; i += 64) lb[i] *= sc;
         __syncthreads();
         STEIN_STAMP(6 + 2 * it);
     }
-    for (int i = lane; i < n; i += 64) Zt[size_t(q) * ldz + i] = lb[i];
+    for (int i = tid; i < n; i += 64 * SW_WAVES) Zt[size_t(q) * ldz + i] = lb[i];
     STEIN_STAMP(11);
 #undef STEIN_STAMP
 }
@@ -879,7 +893,7 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     check_launch("k_sytrd");
     // the chains' reciprocals: 2 Newton steps after the hardware estimate (one step measured 4.40 vs 4.47 ms
     // per cfg3 round(64) but multiplies the kept sigma's relative error by ~20)
-    hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status,
+    hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64 * SW_WAVES), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status,
                        stp ? stp + 768 : nullptr);
     check_launch("k_stebz_stein");
     hipLaunchKernelGGL(k_cluster_orth, dim3(1), dim3(256), 0, h->stream, lm, dbuf.d(), ebuf.d(), n, kk, Ut, ldu);
