@@ -274,8 +274,16 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
 // processed one after the other to bound the live operand registers.
 template <int NR>   // 32-row block rows: 8 (orders <= 256) or 4 (orders <= 128)
 __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
-                                                   double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V) {
+                                                   double* __restrict__ e, double* __restrict__ tau, double* __restrict__ V,
+                                                   unsigned long long* __restrict__ stamps) {
     constexpr int NW = 8, NP = 32 * NR;
+    // diagnostics (stamps != null): threads 0 and 64 record s_memtime at 8 points of the first 64 column steps
+    // (compiled for NR <= 4 only: at NR = 8 the stamp code alone spilled 216 B per lane)
+#define L512_STAMP(p)                                                                                   \
+    do {                                                                                                \
+        if (NR <= 4 && stamps && (threadIdx.x == 0 || threadIdx.x == 64) && j < 64)                      \
+            stamps[(threadIdx.x == 0 ? 0 : 512) + 8 * j + (p)] = __builtin_amdgcn_s_memtime();           \
+    } while (0)
     constexpr int NL = NR * (NR + 1);   // block row ia holds column blocks 0 .. 2 ia + 1: offset ia (ia + 1)
     __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX], psr[SY_MAX], cbuf[NW][SY_MAX];
     __shared__ double sh_tau;
@@ -320,7 +328,9 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
     } while (0)
     L512_PUBLISH(0);
     for (int j = 0; j + 2 < n; ++j) {
+        L512_STAMP(0);
         lds_barrier();
+        L512_STAMP(1);
         if (wave == 0) {   // reflector (dlarfg), as in k_sytrd
             constexpr int E = NP / 64;
             double x[E];
@@ -353,7 +363,9 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                 tau[j] = tv;
             }
         }
+        L512_STAMP(2);
         lds_barrier();
+        L512_STAMP(3);
         // (no early exit for tau = 0: p = w = 0 then and the update leaves every entry unchanged; a second
         // loop latch would double the live matrix registers at the merge)
         const double tj = sh_tau;
@@ -408,14 +420,18 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                 const double r = sum16(rp[ia]);
                 if (tc == 0) psr[tr + 32 * ia] = r;
             }
+            L512_STAMP(4);
             lds_barrier();
+            L512_STAMP(5);
             if (t < SY_MAX) {
                 double c = 0.0;
 #pragma unroll
                 for (int w = 0; w < NW; ++w) c += cbuf[w][t];
                 ps[t] = (t > j && t < n) ? tj * (psr[t] + c) : 0.0;
             }
+            L512_STAMP(6);
             lds_barrier();
+            L512_STAMP(7);
             // K = -(tau / 2) (p . v) in every wave, w = p + K v on the fly; A -= v w^T + w v^T on the kept entries
             double sk = 0.0;
 #pragma unroll
@@ -454,6 +470,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
     }
 #undef L512_PUBLISH
 #undef L512_PUBLISH_CASE
+#undef L512_STAMP
     // the last 2 x 2 block: d[n-2], d[n-1], e[n-2] (tau = 0, H = I)
 #pragma unroll
     for (int ia = 0; ia < NR; ++ia)
@@ -865,8 +882,8 @@ void sym_tridiag(xrs_handle_t h, const double* A, int lda, int n, double* d, dou
     XRS_REQUIRE(n >= 2 && n <= SY_MAX, "sym_tridiag: need 2 <= n <= 256");
     DevBuf tbuf(h, size_t(n) * 8), V(h, size_t(n) * n * 8);
     if (n <= 64) hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
-    else if (n <= 128) hipLaunchKernelGGL(k_sytrd_l512<4>, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d());
-    else hipLaunchKernelGGL(k_sytrd_l512<8>, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d());
+    else if (n <= 128) hipLaunchKernelGGL(k_sytrd_l512<4>, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
+    else hipLaunchKernelGGL(k_sytrd_l512<8>, dim3(1), dim3(512), 0, h->stream, A, lda, n, d, e, tbuf.d(), V.d(), nullptr);
     check_launch("k_sytrd");
 }
 
@@ -876,9 +893,9 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     double* lm = lam ? lam : lbuf.d();
     KernelTimer timer(h, XRS_KFAM_SVD, 4.0 / 3.0 * double(n) * n * n + 4.0 * double(n) * n * kk, 8.0 * double(n) * n * 2);
     static const bool want_stamps = stamps_enabled("syev");
-    DevBuf sb(h, want_stamps ? 1024 * 8 : 0);
+    DevBuf sb(h, want_stamps ? 2048 * 8 : 0);
     unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
-    if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 1024 * 8, h->stream));
+    if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 2048 * 8, h->stream));
     // the 1024-thread grid up to 64 (r04 A/B, profiles/r04/sytrd_l512_ab_r04t.txt: order-64 edges 2.20 vs
     // 2.38 ms per cfg3-shaped round(32) with the 512-thread kernel), the 512-thread lower-block grid with
     // finished-block skipping above (order 128: 4.11 vs 4.58 ms per cfg3 round(64) against the 1024-thread
@@ -886,9 +903,11 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     if (n <= 64) {
         hipLaunchKernelGGL((k_sytrd<32, 2>), dim3(1), dim3(1024), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(), stp);
     } else if (n <= 128) {
-        hipLaunchKernelGGL(k_sytrd_l512<4>, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
+        hipLaunchKernelGGL(k_sytrd_l512<4>, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(),
+                           stp ? stp + 1024 : nullptr);
     } else {
-        hipLaunchKernelGGL(k_sytrd_l512<8>, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d());
+        hipLaunchKernelGGL(k_sytrd_l512<8>, dim3(1), dim3(512), 0, h->stream, A, lda, n, dbuf.d(), ebuf.d(), tbuf.d(), V.d(),
+                           stp ? stp + 1024 : nullptr);
     }
     check_launch("k_sytrd");
     // the chains' reciprocals: 2 Newton steps after the hardware estimate (one step measured 4.40 vs 4.47 ms
@@ -902,6 +921,25 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     else if (n <= 128) hipLaunchKernelGGL((k_ormtr<2>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     else hipLaunchKernelGGL((k_ormtr<4>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
     check_launch("k_ormtr");
+    if (stp && n > 64) {   // k_sytrd_l512 column-step phases (cycles, mean over the first 63 steps)
+        std::vector<unsigned long long> hl(1024);
+        XRS_HIP(hipMemcpyAsync(hl.data(), stp + 1024, 1024 * 8, hipMemcpyDeviceToHost, h->stream));
+        XRS_HIP(hipStreamSynchronize(h->stream));
+        for (int w = 0; w < 2; ++w) {
+            double ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            int steps = 0;
+            for (int j = 0; j + 1 < std::min(n - 2, 64); ++j) {
+                const unsigned long long* a = hl.data() + 512 * w + 8 * j;
+                if (!a[0] || !a[8]) continue;
+                for (int p = 0; p < 7; ++p) ph[p] += double(a[p + 1] - a[p]);
+                ph[7] += double(a[8] - a[7]);
+                ++steps;
+            }
+            std::fprintf(stderr, "k_sytrd_l512 n=%d thread %d: mean cycles per step over %d: barrier1 %.0f reflector %.0f barrier2 %.0f symv %.0f "
+                         "barrier3 %.0f combine %.0f barrier4 %.0f update %.0f\n", n, w ? 64 : 0, steps, ph[0] / steps, ph[1] / steps,
+                         ph[2] / steps, ph[3] / steps, ph[4] / steps, ph[5] / steps, ph[6] / steps, ph[7] / steps);
+        }
+    }
     if (stp) {   // k_stebz_stein phases of workgroup 0 (cycles)
         std::vector<unsigned long long> hs(12);
         XRS_HIP(hipMemcpyAsync(hs.data(), stp + 768, 12 * 8, hipMemcpyDeviceToHost, h->stream));
