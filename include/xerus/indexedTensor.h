@@ -75,6 +75,8 @@ IndexedProduct operator*(const IndexedTensor<Tensor>& _a, const value_t _f);
 IndexedProduct operator*(const value_t _f, IndexedProduct _a);
 IndexedProduct operator*(IndexedProduct _a, const value_t _f);
 IndexedProduct operator/(const IndexedTensor<Tensor>& _a, const value_t _f);
+/// x(i...) = b(j...) / A(j..., i...): the (least-squares) solution of A x = b (indexedTensor_tensor_solve.cpp:31-75)
+IndexedProduct operator/(const IndexedTensor<Tensor>& _b, const IndexedTensor<Tensor>& _A);
 IndexedProduct operator/(IndexedProduct _a, const value_t _f);
 IndexedProduct operator-(const IndexedTensor<Tensor>& _a);
 IndexedProduct operator-(IndexedProduct _a);

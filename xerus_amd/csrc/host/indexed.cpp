@@ -357,6 +357,37 @@ IndexedProduct operator/(IndexedProduct _a, const value_t _f) {
     return _a;
 }
 IndexedProduct operator/(const IndexedTensor<Tensor>& _a, const value_t _f) { return _a.as_product() / _f; }
+
+// x(orderX) = b / A (indexedTensor_tensor_solve.cpp:31-75): A's indices shared with b come first (rows, in A's
+// order), A's others are x's leading indices; b's indices not in A are extra trailing dimensions of both b
+// and x. A and b are reshuffled into that order and solve() (tensor.cpp: LU / least squares) runs on them.
+IndexedProduct operator/(const IndexedTensor<Tensor>& _b, const IndexedTensor<Tensor>& _A) {
+    const std::vector<Index> ia = internal::resolve_indices(_A.indices, _A.tensorObject->degree());
+    const std::vector<Index> ib = internal::resolve_indices(_b.indices, _b.tensorObject->degree());
+    std::vector<Index> orderA, orderB, orderX;
+    size_t extraDims = 0;
+    for (const Index& idx : ia) {
+        if (std::find(ib.begin(), ib.end(), idx) != ib.end()) orderA.push_back(idx);
+        else orderX.push_back(idx);
+    }
+    orderB = orderA;
+    orderA.insert(orderA.end(), orderX.begin(), orderX.end());
+    for (const Index& idx : ib) {
+        if (std::find(ia.begin(), ia.end(), idx) == ia.end()) {
+            orderB.push_back(idx);
+            orderX.push_back(idx);
+            extraDims += idx.span;
+        }
+    }
+    Tensor A, B;
+    A(orderA) << _A.as_product();
+    B(orderB) << _b.as_product();
+    auto X = std::make_shared<Tensor>();
+    solve(*X, A, B, extraDims);
+    IndexedProduct p;
+    p.terms.push_back(IndexedTerm{X, orderX});
+    return p;
+}
 IndexedProduct operator-(IndexedProduct _a) { return -1.0 * std::move(_a); }
 IndexedProduct operator-(const IndexedTensor<Tensor>& _a) { return -1.0 * _a.as_product(); }
 

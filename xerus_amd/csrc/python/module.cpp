@@ -116,6 +116,7 @@ PYBIND11_MODULE(xerus, m) {
         .def("__mul__", [](const IndexedTensor<Tensor>& _a, value_t _f) { return _a * _f; })
         .def("__rmul__", [](const IndexedTensor<Tensor>& _a, value_t _f) { return _f * _a; })
         .def("__truediv__", [](const IndexedTensor<Tensor>& _a, value_t _f) { return _a / _f; })
+        .def("__truediv__", [](const IndexedTensor<Tensor>& _b, const IndexedTensor<Tensor>& _A) { return _b / _A; })
         .def("__neg__", [](const IndexedTensor<Tensor>& _a) { return -_a; })
         .def("__add__", [](const IndexedTensor<Tensor>& _a, const IndexedTensor<Tensor>& _b) { return _a + _b; })
         .def("__add__", [](const IndexedTensor<Tensor>& _a, const IndexedProduct& _b) { return _a + _b; })
