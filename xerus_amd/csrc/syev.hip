@@ -388,10 +388,12 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                     cp[q] = 0.0;
                     vk[q] = vs[tc + 16 * (8 * hh + q)];
                 }
+                double vi_n = vs[tr + 32 * IA0];   // (the next block row's v_i read one block row ahead)
 #pragma unroll
                 for (int ia = IA0; ia < NR; ++ia) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    const double vi = vs[tr + 32 * ia];
+                    if constexpr (NR > 4) __builtin_amdgcn_sched_barrier(0);
+                    const double vi = vi_n;
+                    if (ia + 1 < NR) vi_n = vs[tr + 32 * (ia + 1)];
 #pragma unroll
                     for (int q = 0; q < 8; ++q) {
                         const int ib = 8 * hh + q;
@@ -443,11 +445,18 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                 vi[ia] = vs[tr + 32 * ia];
                 wi[ia] = fma(K, vi[ia], ps[tr + 32 * ia]);
             }
+            // one column block at a time at NR = 8 (hoisted operands spill there), its operands read one
+            // block ahead; NR <= 4 leaves the scheduling to the compiler
+            double vk_n = vs[tc + 32 * IA0], pk_n = ps[tc + 32 * IA0];
 #pragma unroll
             for (int ib = 2 * IA0; ib < 2 * NR; ++ib) {
-                __builtin_amdgcn_sched_barrier(0);   // one column block at a time (hoisted operands spill)
-                const double vk = vs[tc + 16 * ib];
-                const double wk = fma(K, vk, ps[tc + 16 * ib]);
+                if constexpr (NR > 4) __builtin_amdgcn_sched_barrier(0);
+                const double vk = vk_n, pk = pk_n;
+                if (ib + 1 < 2 * NR) {
+                    vk_n = vs[tc + 16 * (ib + 1)];
+                    pk_n = ps[tc + 16 * (ib + 1)];
+                }
+                const double wk = fma(K, vk, pk);
 #pragma unroll
                 for (int ia = (ib / 2 > IA0 ? ib / 2 : IA0); ia < NR; ++ia) {
                     const int ix = ia * (ia + 1) + ib;

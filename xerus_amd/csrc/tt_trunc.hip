@@ -168,10 +168,11 @@ void orth_devs(Sweep& sw, const std::vector<const double*>& X, const std::vector
 // wide edge, B = L Q with the left singular vectors of L as the rows of Ut (Jacobi on the columns of L):
 // M = S^{-1} Ut[:kk] (new core = M B = Vt_kk Q) and T = Ut[:kk]^T S (= U S, core_{k-1} <- core_{k-1} T)
 __global__ void __launch_bounds__(256) k_edge_factors(const double* __restrict__ Ut, const double* __restrict__ S, int r, int kk,
-                                                      double* __restrict__ M, double* __restrict__ T) {
+                                                      double* __restrict__ M, double* __restrict__ T, int s_is_lam) {
     for (int e = blockIdx.x * 256 + threadIdx.x; e < kk * r; e += gridDim.x * 256) {
         const int i = e / r, j = e - i * r;
-        const double u = Ut[size_t(i) * r + j], s = S[i];
+        // (s_is_lam: S holds the eigenvalues of P = B B^T, sigma = sqrt(max(lambda, 0)) -- k_sqrt_lam's value)
+        const double u = Ut[size_t(i) * r + j], s = s_is_lam ? sqrt(fmax(S[i], 0.0)) : S[i];
         M[e] = s > 0.0 ? u / s : 0.0;
         T[size_t(j) * kk + i] = u * s;
     }
@@ -324,6 +325,18 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     // handle owns its streams and is not inside a fork
     const bool cert_side = !h->borrowed_streams && h->stream == h->own_stream && h->side_stream[0] && h->prof_mask == 0;
     bool side_used = false;
+    struct : PotrfBatch { int count = 0; } pending_cert{};
+    auto flush_certs = [&]() {
+        if (pending_cert.count == 0) return;
+        pending_cert.status = status + nst;
+        XRS_HIP(hipEventRecord(h->ev_fork, h->stream));
+        XRS_HIP(hipStreamWaitEvent(h->side_stream[0], h->ev_fork, 0));
+        side_used = true;
+        StreamSwap on_side(h, h->side_stream[0]);   // (restores h->stream on scope exit, also on a throw)
+        potrf_batched(h, pending_cert, pending_cert.count);
+        nst += pending_cert.count;
+        pending_cert.count = 0;
+    };
     for (size_t k = d - 1; k >= 1; --k) {
         const size_t r = rr[k], N = t.n[k] * rr[k + 1], Ng = ng[k] * rr[k + 1];   // local / global columns
         const size_t kk = std::min({r, Ng, max_ranks[k - 1]});
@@ -353,22 +366,19 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         double* L = use_eig ? nullptr : sw.buf(g * g);
         double* Z = (!use_eig && g > 256) ? sw.buf(g * g) : nullptr;   // (factor_big always builds L^{-1})
         if (use_eig && cert_side) {
-            // the eigensolver does not need the factor: the status-only certificate runs on a side stream
-            // beside it (its status is read after the one join before the final check)
-            double* dinv = sw.buf(dinv_elems(int(g)));
-            PotrfBatch pb{};
-            pb.src[0] = P;
-            pb.G[0] = nullptr;
-            pb.Dinv[0] = dinv;
-            pb.shift[0] = -kGramShift;
-            pb.n[0] = int(g);
-            pb.status = status + nst;
-            XRS_HIP(hipEventRecord(h->ev_fork, h->stream));
-            XRS_HIP(hipStreamWaitEvent(h->side_stream[0], h->ev_fork, 0));
-            side_used = true;
-            StreamSwap on_side(h, h->side_stream[0]);   // (restores h->stream on scope exit, also on a throw)
-            potrf_batched(h, pb, 1);
-            nst += 1;
+            // the eigensolver does not need the factor: the status-only certificates run on a side stream
+            // beside it (their statuses are read after the one join before the final check), batched: edges
+            // d-1 .. 2 in one launch forked behind edge 2's P, edge 1 on its own (a fork per edge left a
+            // ~7 us gap before every tridiagonalisation: the event record on the main stream)
+            const int slot = pending_cert.count;
+            XRS_REQUIRE(slot < kPotrfBatchMax, "round_truncate: too many certificates");
+            pending_cert.src[slot] = P;
+            pending_cert.G[slot] = nullptr;
+            pending_cert.Dinv[slot] = sw.buf(dinv_elems(int(g)));
+            pending_cert.shift[slot] = -kGramShift;
+            pending_cert.n[slot] = int(g);
+            pending_cert.count = slot + 1;
+            if (k <= 2 || slot + 1 == kPotrfBatchMax) flush_certs();
         } else {
             std::vector<CholJob> cj{{P, int(g), nullptr, nullptr}};
             if (!use_eig) cj.insert(cj.begin(), CholJob{P, int(g), L, Z});
@@ -378,7 +388,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         double* S = sw.buf(g);
         double* Vt = wide ? sw.buf(g * g) : sw.core(g * g);
         int* js = status + kJacobiSlot + int(jst.size());
-        if (use_eig) sym_eig_top(h, P, int(g), int(g), int(kk), nullptr, S, Vt, int(g), js);
+        if (use_eig) sym_eig_top(h, P, int(g), int(g), int(kk), S, nullptr, Vt, int(g), js);   // (S <- lambda)
         else jacobi_vt(h, L, int(g), true, int(g), int(g), S, Vt, int(g), js);
         jst.push_back(js);
         double* Tk = sw.buf(r * kk);
@@ -386,7 +396,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         if (wide) {   // Vt holds U_L^T (P = B B^T = L L^T, B = L Q, L = U S V^T)
             double* M = sw.buf(kk * r);
             hipLaunchKernelGGL(k_edge_factors, dim3(unsigned(std::min<size_t>((kk * r + 255) / 256, 512))), dim3(256), 0,
-                               h->stream, Vt, S, int(r), int(kk), M, Tk);
+                               h->stream, Vt, S, int(r), int(kk), M, Tk, int(use_eig));
             check_launch("k_edge_factors");
             newk = sw.core(kk * N);
             gemm(h, newk, kk, N, 1.0, M, r, false, r, B, N, false);               // S^{-1} U^T B = Vt_B[:kk]
@@ -403,6 +413,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         A[k - 1] = prevk;
         rr[k] = kk;
     }
+    flush_certs();
     if (side_used) {   // join: the side stream's certificates before the statuses are read
         XRS_HIP(hipEventRecord(h->ev_join[0], h->side_stream[0]));
         XRS_HIP(hipStreamWaitEvent(h->stream, h->ev_join[0], 0));
