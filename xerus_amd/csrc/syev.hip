@@ -267,10 +267,10 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
 // Orders 129..256: the same column steps on 512 threads (8 waves, two per SIMD: 256 VGPRs each) holding
 // the lower triangle by blocks. Thread (tr, tc) = (t / 16, t % 16) of a 32 x 16 grid owns the elements
 // (tr + 32 ia, tc + 16 ib) of the blocks with ib <= 2 ia + 1 (the ones meeting the lower triangle:
-// 72 doubles); the entries above the diagonal in the two diagonal-crossing blocks of a block row stay zero.
-// The symmetric product sums the rows of the stored entries (over the 16 column threads of a row: one DPP
-// row) plus, for the mirrored upper triangle, the columns of the strictly lower ones (over the 4 rows of a
-// wave by permlane16 / shuffle, then over the 8 waves through LDS). The column halves (ib < 8, ib >= 8) are
+// 72 doubles); the two diagonal-crossing blocks of a block row (its 32 x 32 diagonal square) hold both
+// triangles. The symmetric product sums the rows of the stored entries (over the 16 column threads of a
+// row: one DPP row) plus, for the mirrored upper triangle outside the squares, the columns of the strictly
+// lower blocks (over the 4 rows of a wave by permlane16 / shuffle, then over the 8 waves through LDS). The column halves (ib < 8, ib >= 8) are
 // processed one after the other to bound the live operand registers.
 template <int NR>   // 32-row block rows: 8 (orders <= 256) or 4 (orders <= 128)
 __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A, int lda, int n, double* __restrict__ d,
@@ -288,18 +288,20 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
     __shared__ double xs[SY_MAX], vs[SY_MAX], ps[SY_MAX], psr[SY_MAX], cbuf[NW][SY_MAX];
     __shared__ double sh_tau;
     const int t = threadIdx.x, tr = t >> 4, tc = t & 15, lane = t & 63, wave = t >> 6;
-    // diagonal-crossing blocks of block row ia: ib = 2 ia (i - k = tr - tc), ib = 2 ia + 1 (i - k = tr - tc - 16)
-    const bool keep0 = tr >= tc, keep1 = tr >= tc + 16;   // on or below the diagonal
-    const bool low0 = tr > tc, low1 = tr > tc + 16;       // strictly below
+    // the 32 x 32 diagonal squares (blocks 2 ia, 2 ia + 1 of block row ia) hold BOTH triangles (the upper
+    // entries are the mirrored values, kept by the same rank-2 update): no masks in the symmetric product or
+    // the update; the product's row sums run over every stored entry, its column (mirror) sums over the
+    // strictly lower blocks ib < 2 ia only
     double a[NL];
 #pragma unroll
     for (int ia = 0; ia < NR; ++ia)
 #pragma unroll
         for (int ib = 0; ib <= 2 * ia + 1; ++ib) {
             const int i = tr + 32 * ia, k = tc + 16 * ib;
-            const bool keep = (ib < 2 * ia || (ib == 2 * ia ? keep0 : keep1)) && i < n && k < n;
-            const double x = A[size_t(keep ? i : 0) * lda + (keep ? k : 0)];
-            a[ia * (ia + 1) + ib] = keep ? x : 0.0;
+            const bool in = i < n && k < n;
+            const int r = i >= k ? i : k, c = i >= k ? k : i;   // (A is read from its lower triangle)
+            const double x = A[size_t(in ? r : 0) * lda + (in ? c : 0)];
+            a[ia * (ia + 1) + ib] = in ? x : 0.0;
         }
     // column jj of the current matrix to LDS (xs) and its diagonal entry to d, by the column's owners
 #define L512_PUBLISH_CASE(IB)                                                             \
@@ -401,13 +403,13 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                             const double av = a[ia * (ia + 1) + ib];
                             rp[ia] = fma(av, vk[q], rp[ia]);
                             if (ib < 2 * ia) cp[q] = fma(av, vi, cp[q]);
-                            else cp[q] = fma((ib == 2 * ia ? low0 : low1) ? av : 0.0, vi, cp[q]);
                         }
                     }
                 }
 #pragma unroll
                 for (int q = 0; q < 8; ++q) {
-                    if (8 * hh + q < 2 * IA0) continue;
+                    // (column blocks of the last square have no strictly lower block: cp = 0)
+                    if (8 * hh + q < 2 * IA0 || 8 * hh + q >= 2 * NR - 2) continue;
                     cp[q] += xor16(cp[q]);
                     cp[q] += xor32(cp[q]);
                 }
@@ -460,8 +462,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 #pragma unroll
                 for (int ia = (ib / 2 > IA0 ? ib / 2 : IA0); ia < NR; ++ia) {
                     const int ix = ia * (ia + 1) + ib;
-                    const double u = fma(-vi[ia], wk, fma(-wi[ia], vk, a[ix]));
-                    a[ix] = (ib < 2 * ia || (ib == 2 * ia ? keep0 : keep1)) ? u : 0.0;
+                    a[ix] = fma(-vi[ia], wk, fma(-wi[ia], vk, a[ix]));
                 }
             }
         };
