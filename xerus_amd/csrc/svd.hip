@@ -37,14 +37,6 @@ __device__ __forceinline__ double dpp(double v) {
     return __hiloint2double(hi, lo);
 }
 
-// The value of lane l ^ 16 (the other DPP row of a 32-lane group) by gfx950's v_permlane16_swap (a VALU
-// exchange of odd and even 16-lane rows; __shfl_xor goes through the LDS crossbar)
-__device__ __forceinline__ double xor16(double v) {
-    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
-    // odd rows receive the even rows in the first result, even rows the odd rows in the second
-    return (threadIdx.x & 16) ? __hiloint2double(hi[0], lo[0]) : __hiloint2double(hi[1], lo[1]);
-}
 
 // Sum over a group of G (8, 16 or 32) consecutive lanes. Every lane of the group ends with the same bits:
 // each step adds two values that are equal up to the order of operands of commutative adds.
@@ -57,7 +49,12 @@ __device__ __forceinline__ double gsum(double v) {
         v += dpp<0x124>(v);
         v += dpp<0x122>(v);
         v += dpp<0x121>(v);
-        if constexpr (G == 32) v += xor16(v);   // the two DPP rows of the group
+        if constexpr (G == 32) {   // the two DPP rows of the group: the two results of v_permlane16_swap(v, v)
+            // are {own, partner} on every lane, so their sum is the pair sum without a per-lane select
+            const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+            const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+            v = __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+        }
     } else {
         static_assert(G == 8, "groups of 8 or 16 lanes");
         v += dpp<0x141>(v);

@@ -50,11 +50,6 @@ __device__ __forceinline__ double dpp(double v) {
     const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double xor16(double v) {
-    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
-    return (threadIdx.x & 16) ? __hiloint2double(hi[0], lo[0]) : __hiloint2double(hi[1], lo[1]);
-}
 __device__ __forceinline__ double sum16(double v) {   // every lane of the 16-lane row gets the row's sum
     v += dpp<0x128>(v);
     v += dpp<0x124>(v);
@@ -62,13 +57,21 @@ __device__ __forceinline__ double sum16(double v) {   // every lane of the 16-la
     v += dpp<0x121>(v);
     return v;
 }
-__device__ __forceinline__ double sum32(double v) { v = sum16(v); return v + xor16(v); }
-__device__ __forceinline__ double xor32(double v) {   // the value of lane l ^ 32 (v_permlane32_swap)
+// v + (the value of lane l ^ 16): the two results of v_permlane16_swap(v, v) are {own, partner} on every lane
+// (odd rows get the even rows in the first, even rows the odd rows in the second), so their sum is the pair
+// sum without the per-lane select -- one dependent operation less per level, bit-identical (a + b = b + a)
+__device__ __forceinline__ double addx16(double v) {
+    const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double addx32(double v) {   // v + (the value of lane l ^ 32), v_permlane32_swap
     const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
     const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
-    return (threadIdx.x & 32) ? __hiloint2double(hi[0], lo[0]) : __hiloint2double(hi[1], lo[1]);
+    return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
 }
-__device__ __forceinline__ double sum64(double v) { v = sum32(v); return v + xor32(v); }
+__device__ __forceinline__ double sum32(double v) { return addx16(sum16(v)); }
+__device__ __forceinline__ double sum64(double v) { return addx32(sum32(v)); }
 
 // workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
 // stores (__syncthreads' release fence would drain the per-column stores of the reflectors, d, e and tau
@@ -199,7 +202,7 @@ __global__ void __launch_bounds__(GRID * GRID) k_sytrd(const double* __restrict_
             for (int ia = 0; ia < NB; ++ia) part[ia] += dpp<0x121>(part[ia]);
             if constexpr (GRID == 32) {
 #pragma unroll
-                for (int ia = 0; ia < NB; ++ia) part[ia] += xor16(part[ia]);
+                for (int ia = 0; ia < NB; ++ia) part[ia] = addx16(part[ia]);
             }
             if (tc == 0) {
 #pragma unroll
@@ -410,8 +413,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
                 for (int q = 0; q < 8; ++q) {
                     // (column blocks of the last square have no strictly lower block: cp = 0)
                     if (8 * hh + q < 2 * IA0 || 8 * hh + q >= 2 * NR - 2) continue;
-                    cp[q] += xor16(cp[q]);
-                    cp[q] += xor32(cp[q]);
+                    cp[q] = addx32(addx16(cp[q]));
                 }
                 if (lane < 16) {
 #pragma unroll
