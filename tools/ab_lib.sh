@@ -1,9 +1,13 @@
-# A/B of two builds of libxerus_amd.so on one box: abtmp/old.so (XRS_LIB_PATH) against the in-tree build,
-# alternating. Usage: bash tools/ab_lib.sh OUTDIR [env for tools/trunc_profile.py, e.g. "RANK=128 TARGET=64"]
+# A/B of library builds on one box: every abtmp/<name>.so (XRS_LIB_PATH; name "old" = the baseline) and the
+# in-tree build ("new"), alternating, 3 rounds. Usage: bash tools/ab_lib.sh OUTDIR [env for
+# tools/trunc_profile.py, e.g. "RANK=128 TARGET=64"]
 set -e
 O=$1; shift; mkdir -p $O
 for k in 1 2 3; do
-  env $@ XRS_LIB_PATH=$PWD/abtmp/old.so REPS=8 timeout -k 10 120 python tools/trunc_profile.py > $O/old_$k.txt 2>&1
+  for lib in abtmp/*.so; do
+    b=$(basename $lib .so)
+    env $@ XRS_LIB_PATH=$PWD/$lib REPS=8 timeout -k 10 120 python tools/trunc_profile.py > $O/${b}_$k.txt 2>&1
+  done
   env $@ REPS=8 timeout -k 10 120 python tools/trunc_profile.py > $O/new_$k.txt 2>&1
 done
-tail -n 3 $O/old_*.txt $O/new_*.txt
+tail -n 3 $O/*_[123].txt
