@@ -462,6 +462,20 @@ def main():
     for _ in range(args.steps):
         step_seq(timing)
     barrier()
+    # side key (not the headline, which stays f64 like the reference's value_t): the same <x,y> on fp32 MFMA
+    # tiles (xrs_tt_dot_f32), host-timed per call like dot_ms, and its error against the f64 product
+    d64 = x.dot(y)
+    d32 = x.dot_f32(y)
+    for _ in range(2):
+        x.dot_f32(y)
+    barrier()
+    t32 = time.perf_counter()
+    for _ in range(args.steps):
+        x.dot_f32(y)
+    t32 = (time.perf_counter() - t32) / args.steps
+    dot_f32 = {"ms": round(t32 * 1e3, 4), "tflops": round(f_dot / t32 / 1e12, 3),
+               "rel_err": abs(d32 - d64) / (x.frob_norm() * y.frob_norm()),
+               "path": "xrs_tt_dot_f32: two-ended zipper, v_mfma_f32_16x16x4_f32, fp64 cores rounded at load"}
 
     # Roofline passes: the same K steps again with a HIP event pair on every GEMM launch (the start / stop
     # events of hipExtLaunchKernelGGL on the stream each launch goes to: the dispatch's own begin / end
@@ -615,6 +629,7 @@ def main():
                 "step": ("sequential: x.dot(y), then x.round" if args.no_overlap else
                          "overlapped: x.dot_async(y) on side streams beside x.round on the main stream, both waited for"),
                 "dot_ms": round(timing["dot"] / args.steps * 1e3, 4),
+                "dot_f32": dot_f32,
                 "round_sweep_ms": round(timing["round"] / args.steps * 1e3, 4),
                 "sequential_ms_per_step": round((timing["dot"] + timing["round"]) / args.steps * 1e3, 4),
                 "gflop_per_step": round(f_step / 1e9, 4),

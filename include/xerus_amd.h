@@ -222,6 +222,14 @@ int xrs_tt_dot_async(xrs_handle_t handle, size_t d, const size_t* n,
                      const size_t* ry, const double* const* ycores);
 /** Waits for the handle's asynchronous inner product; *result on host. */
 int xrs_tt_dot_wait(xrs_handle_t handle, double* result);
+/** <x,y> on fp32 MFMA tiles (v_mfma_f32_16x16x4_f32): the two-ended zipper of xrs_tt_dot with the fp64
+ *  cores rounded to fp32 as they are loaded, fp32 environments renormalised by powers of two every step,
+ *  the closing sum in fp64. A reduced-precision side path (|error| ~1e-7 ||x|| ||y||), NOT a replacement
+ *  for value_t(x(i&0)*y(i&0)) (ttNetwork.cpp:782-789), which xrs_tt_dot restates in fp64. d >= 2.
+ *  *result on host. Synchronises. */
+int xrs_tt_dot_f32(xrs_handle_t handle, double* result, size_t d, const size_t* n,
+                   const size_t* rx, const double* const* xcores,
+                   const size_t* ry, const double* const* ycores);
 
 /** All-reduce (element-wise sum over all ranks) of `count` doubles at the device pointer `buf`, in place.
  *  Called by the sharded TT entry points with the handle's stream synchronised; returns 0 on success.

@@ -67,6 +67,8 @@ SIGNATURES = {
     "xrs_tt_dot_async": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
                                    C.POINTER(_DP)]),
     "xrs_tt_dot_wait": (C.c_int, [_DP, C.POINTER(C.c_double)]),
+    "xrs_tt_dot_f32": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
+                                 C.POINTER(_SZ), C.POINTER(_DP)]),
     "xrs_tt_round_sharded": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
                                        C.c_double, _DP, _DP, C.POINTER(C.c_int)]),
     "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
@@ -517,6 +519,17 @@ class TTDevice:
         n, rx, xc = self._arrays()
         _, ry, yc = other._arrays()
         _check("xrs_tt_dot", self.handle.lib.xrs_tt_dot(self.handle.h, C.byref(out), self.order, n, rx, xc, ry, yc))
+        return out.value
+
+    def dot_f32(self, other: "TTDevice") -> float:
+        """<self, other> on fp32 MFMA tiles (xrs_tt_dot_f32): a reduced-precision side path, error ~1e-7
+        ||self|| ||other||; dot() is the fp64 product the reference computes."""
+        if self.dims != other.dims:
+            raise ValueError(f"dot of TTs with different dimensions: {self.dims} vs {other.dims}")
+        out = C.c_double()
+        n, rx, xc = self._arrays()
+        _, ry, yc = other._arrays()
+        _check("xrs_tt_dot_f32", self.handle.lib.xrs_tt_dot_f32(self.handle.h, C.byref(out), self.order, n, rx, xc, ry, yc))
         return out.value
 
     def dot_async(self, other: "TTDevice") -> "DotFuture":
