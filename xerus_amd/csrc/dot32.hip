@@ -229,7 +229,8 @@ __global__ void __launch_bounds__(256) k_pair_dot(const float* __restrict__ E, c
     if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
-// split-K slice count for an M x N x K product: about 320 workgroups over the chip, whole 32-deep steps
+// split-K slice count for an M x N x K product: about 320 workgroups, whole 32-deep steps (160 / 640
+// measured the same within the box spread: profiles/r04/dot32_split_ab_r04be.txt)
 int splits_for(int M, int N, int K) {
     const int tiles = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     int s = std::max(1, std::min(320 / tiles, (K + 4 * BK - 1) / (4 * BK)));   // >= 4 steps per slice
