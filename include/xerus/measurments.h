@@ -25,6 +25,7 @@ class SinglePointMeasurementSet {
     static SinglePointMeasurementSet random(const size_t _numMeasurements, const std::vector<size_t>& _dimensions);
     static SinglePointMeasurementSet random(const size_t _numMeasurements, const Tensor& _solution);
     static SinglePointMeasurementSet random(const size_t _numMeasurements, const TTTensor& _solution);
+    static SinglePointMeasurementSet random(const size_t _numMeasurements, const TensorNetwork& _solution);
     static SinglePointMeasurementSet random(const size_t _numMeasurements, const std::vector<size_t>& _dimensions,
                                             std::function<value_t(const std::vector<size_t>&)> _callback);
 
@@ -39,11 +40,15 @@ class SinglePointMeasurementSet {
     void measure(const Tensor& _solution);
     /// all positions at once on the GPU (the core-by-core evaluation stack of the ADF solver)
     void measure(const TTTensor& _solution);
+    /// entry by entry through TensorNetwork::operator[] (the reference's fixed-mode stack, measurments.cpp:125-173,
+    /// computes the same values sharing prefixes)
+    void measure(const TensorNetwork& _solution);
     void measure(std::function<value_t(const std::vector<size_t>&)> _callback);
 
     /// ||values - solution[positions]|| / ||values|| (measurments.cpp:151-199)
     double test(const Tensor& _solution) const;
     double test(const TTTensor& _solution) const;
+    double test(const TensorNetwork& _solution) const;
     double test(std::function<value_t(const std::vector<size_t>&)> _callback) const;
 
    private:

@@ -11,6 +11,18 @@
 
 namespace xerus {
 
+class TensorNetwork;
+
+/// T(i,j,...) = A(...) * B(...) for a TensorNetwork T: the product kept as a network (no contraction), its
+/// external modes in the order of T's indices (the reference's IndexedTensor<TensorNetwork> assignment,
+/// indexedTensorWritable.cpp:68-119 with tensorNetwork.cpp:224-296).
+struct IndexedNetwork {
+    TensorNetwork* network;
+    std::vector<Index> indices;
+    IndexedNetwork& operator=(const IndexedProduct& _rhs);
+    IndexedNetwork& operator=(const IndexedTensor<Tensor>& _rhs);
+};
+
 class TensorNetwork {
    public:
     struct Link {
@@ -68,6 +80,15 @@ class TensorNetwork {
     /// Estimated flops (m*n*r) of contracting everything in the heuristic's order.
     double contraction_cost(const std::set<size_t>& _ids) const;
 
+    /// Entry at a flat / multi index (tensorNetwork.cpp:310-370): every node's external modes are fixed to the
+    /// position (Tensor::fix_mode on the GPU), the remaining network is contracted to a scalar.
+    value_t operator[](const size_t _position) const;
+    value_t operator[](const std::vector<size_t>& _positions) const;
+
+    IndexedNetwork operator()(const std::vector<Index>& _indices) { return IndexedNetwork{this, _indices}; }
+    template <class... args>
+    IndexedNetwork operator()(args... _args) { return IndexedNetwork{this, std::vector<Index>{_args...}}; }
+
     void require_valid_network() const;
     void sanitize();   // drop erased nodes, renumber
 };
@@ -75,6 +96,8 @@ class TensorNetwork {
 class TTTensor;
 
 namespace internal {
+/// the network of a product with its externals in the order of _out (IndexedNetwork's assignment)
+TensorNetwork product_network(const IndexedProduct& _p, const std::vector<Index>& _out);
 /// best greedy contraction order over the reference's five score functions (contractionHeuristic.cpp)
 std::vector<std::pair<size_t, size_t>> greedy_contraction_order(const TensorNetwork& _net, double* _cost = nullptr);
 /// the 2d+4-node network of value_t(x(i&0) * y(i&0)) in the reference's numbering (x: ghost 0, cores

@@ -102,6 +102,15 @@ int xrs_gemm_sym(xrs_handle_t handle, double* C, size_t N, double alpha,
                  const double* A, size_t lda, int transA, size_t K,
                  const double* B, size_t ldb, int transB);
 
+/** fp32 form of xrs_gemm on the fp32 matrix cores (v_mfma_f32_16x16x4_f32, 157.3 TF/s peak): C = alpha *
+ *  op(A) * op(B), float operands and result, row-major, ldc = N; argument order, ld rules and aliasing as
+ *  xrs_gemm. The reduced-precision variant of blasWrapper::matrix_matrix_product (blasLapackWrapper.cpp:
+ *  149-195, whose cblas_dgemm :177-191 computes in value_t = double): relative error ~1e-7 * sum|a b| per
+ *  element. Deterministic (fixed split-K slice order). No reference counterpart at this precision. */
+int xrs_gemm_f32(xrs_handle_t handle, float* C, size_t M, size_t N, float alpha,
+                 const float* A, size_t lda, int transA, size_t K,
+                 const float* B, size_t ldb, int transB);
+
 /* ---------------------------------------------------------------- permutation (tensor.h:65) */
 /** out = reshuffle(in, shuffle): out[...] with mode i of `in` moved to position shuffle[i]
  *  (indexedTensor_tensor_evaluate.cpp:55-143; shuffle[i] = NEW position of OLD mode i, :80-82).

@@ -41,7 +41,8 @@ SIGNATURES = {
     "xrs_axpy": (C.c_int, [_DP, _DP, C.c_double, _DP, _SZ]),
     "xrs_scale_rows": (C.c_int, [_DP, _DP, _DP, _SZ, _SZ]),
     "xrs_gemm": (C.c_int, [_DP, _DP, _SZ, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
-    "xrs_gemm_sym": (C.c_int, [_DP, _DP, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
+    "xrs_gemm_f32": (C.c_int, [_DP, _DP, _SZ, _SZ, C.c_float, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
+    "xrs_gemm_sym": (C.c_int,[_DP, _DP, _SZ, C.c_double, _DP, _SZ, C.c_int, _SZ, _DP, _SZ, C.c_int]),
     "xrs_gemm_batched": (C.c_int, [_DP, _SZ, C.POINTER(_DP), _SZ, _SZ, C.c_double, C.POINTER(_DP), _SZ, C.c_int, _SZ,
                                    C.POINTER(_DP), _SZ, C.c_int]),
     "xrs_permute": (C.c_int, [_DP, _DP, _DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
@@ -183,6 +184,14 @@ class Handle:
     def gemm(self, C_: "DeviceArray", M, N, alpha, A: "DeviceArray", lda, transA, K, B: "DeviceArray", ldb, transB):
         _check("xrs_gemm", self.lib.xrs_gemm(self.h, _DP(C_.ptr), M, N, alpha, _DP(A.ptr), lda, int(transA), K,
                                             _DP(B.ptr), ldb, int(transB)))
+
+    def gemm_f32(self, C_: "Float32Array", M, N, alpha, A: "Float32Array", lda, transA, K, B: "Float32Array", ldb, transB):
+        """xrs_gemm_f32: the fp32-MFMA GEMM on Float32Array operands."""
+        _check("xrs_gemm_f32", self.lib.xrs_gemm_f32(self.h, _DP(C_.ptr), M, N, float(alpha), _DP(A.ptr), lda, int(transA),
+                                                    K, _DP(B.ptr), ldb, int(transB)))
+
+    def array_f32(self, a: np.ndarray) -> "Float32Array":
+        return Float32Array.from_host(self, a)
 
     def gemm_sym(self, C_: "DeviceArray", N, alpha, A: "DeviceArray", lda, transA, K, B: "DeviceArray", ldb, transB):
         _check("xrs_gemm_sym", self.lib.xrs_gemm_sym(self.h, _DP(C_.ptr), N, alpha, _DP(A.ptr), lda, int(transA), K,
@@ -379,6 +388,49 @@ class DeviceArray:
         if self.owned and self.ptr:
             self.handle.free(self.ptr)
         self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Float32Array:
+    """A row-major float32 array in the handle's device pool (operands of xrs_gemm_f32). The C-ABI's
+    upload / download move doubles, so the float32 payload travels as doubles' bytes (padded to 8 B);
+    `offset` (floats) views the array at an unaligned start, to exercise the scalar staging path."""
+
+    def __init__(self, handle: Handle, shape: tuple, offset: int = 0):
+        self.handle = handle
+        self.shape = tuple(int(s) for s in shape)
+        self.offset = int(offset)
+        self._words = max(1, (self.size + self.offset + 1) // 2)
+        self.base = handle.malloc(8 * self._words)
+        self.ptr = self.base + 4 * self.offset
+
+    @property
+    def size(self) -> int:
+        return int(np.prod(self.shape)) if self.shape else 1
+
+    @classmethod
+    def from_host(cls, handle: Handle, a: np.ndarray, offset: int = 0) -> "Float32Array":
+        a = np.ascontiguousarray(a, dtype=np.float32)
+        d = cls(handle, a.shape, offset)
+        buf = np.zeros(2 * d._words, dtype=np.float32)
+        buf[d.offset:d.offset + a.size] = a.ravel()
+        _check("xrs_upload", handle.lib.xrs_upload(handle.h, _DP(d.base), buf.view(np.float64).ctypes.data_as(_DP), d._words))
+        return d
+
+    def numpy(self) -> np.ndarray:
+        buf = np.empty(self._words, dtype=np.float64)
+        _check("xrs_download", self.handle.lib.xrs_download(self.handle.h, buf.ctypes.data_as(_DP), _DP(self.base), self._words))
+        return buf.view(np.float32)[self.offset:self.offset + self.size].reshape(self.shape).copy()
+
+    def free(self):
+        if self.base:
+            self.handle.free(self.base)
+        self.base = self.ptr = 0
 
     def __del__(self):
         try:

@@ -9,8 +9,8 @@
 //   TTNetwork     (ttNetwork.cpp:1455-1487):     version 1, canonicalized, corePosition, TensorNetwork
 // A TTTensor is written with the reference's node layout (ghost ones({1}) node 0, components 1..d, ghost
 // node d+1, ttNetwork.cpp:57-108), so files interchange with the reference in both directions. Device data
-// crosses PCIe only here (explicit host boundary). Sparse payloads (representation 2) are not supported:
-// the build is dense-only.
+// crosses PCIe only here (explicit host boundary). Sparse payloads (representation 2, the reference's files of
+// sparse tensors) are read into dense tensors; files are written dense (the build is dense-only).
 #include <cstdint>
 #include <fstream>
 #include <iomanip>
@@ -83,13 +83,27 @@ struct Reader {
         XERUS_REQUIRE(ver == 1, "Unknown stream version to open (" << ver << ")");
         Tensor::DimensionTuple dims = get_dims();
         const size_t rep = get<size_t>();
-        XERUS_REQUIRE(rep == 1, "Unknown tensor representation " << rep << " in stream (this build reads dense tensors only)");
+        XERUS_REQUIRE(rep == 1 || rep == 2, "Unknown tensor representation " << rep << " in stream");
         // a malformed size must not wrap: check every product, and (binary) that the payload is in the stream
         size_t n = 1;
         for (size_t d : dims) {
             XERUS_REQUIRE(d == 0 || n <= (std::numeric_limits<size_t>::max() / sizeof(value_t)) / d,
                           "Malformed stream: the tensor size overflows");
             n *= d;
+        }
+        if (rep == 2) {
+            // sparse payload (tensor.cpp:1796-1803 / 1826-1840): entry count, then (flat position, value) pairs
+            // with the factor applied; read into a dense tensor (this build's only representation)
+            const size_t num = get<size_t>();
+            XERUS_REQUIRE(num <= n, "Malformed stream: " << num << " sparse entries for " << n << " positions");
+            std::unique_ptr<value_t[]> data(new value_t[std::max<size_t>(n, 1)]());
+            for (size_t i = 0; i < num; ++i) {
+                const size_t pos = get<size_t>();
+                const value_t val = get<value_t>();
+                XERUS_REQUIRE(pos < n, "Malformed stream: sparse position " << pos << " beyond " << n);
+                data[pos] = val;
+            }
+            return Tensor(std::move(dims), std::move(data));
         }
         if (f != FileFormat::TSV) {
             const std::streampos here = s.tellg();

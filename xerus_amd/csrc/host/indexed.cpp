@@ -229,6 +229,66 @@ value_t contract_unconnected(TensorNetwork& _net) {
 
 std::vector<Index> resolve_indices(const std::vector<Index>& _indices, size_t _degree) { return resolve(_indices, _degree); }
 
+// external slot -> position in the output index order (indexedTensorWritable.cpp:97-118)
+static std::vector<size_t> output_slots(const Lowered& L, const std::vector<Index>& _out) {
+    const size_t E = L.net.degree();
+    const std::vector<Index> out = resolve(_out, E);
+    std::vector<size_t> slotOf(E);
+    std::vector<size_t> firstSlot(L.openIndices.size());
+    size_t s = 0;
+    for (size_t k = 0; k < L.openIndices.size(); ++k) {
+        firstSlot[k] = s;
+        s += L.openIndices[k].span;
+    }
+    std::vector<char> used(L.openIndices.size(), 0);
+    size_t pos = 0;
+    for (const Index& I : out) {
+        XERUS_REQUIRE(!I.fixed(), "Traces and fixed indices are not allowed in the target of evaluation.");
+        size_t k = 0;
+        while (k < L.openIndices.size() && L.openIndices[k] != I) ++k;
+        XERUS_REQUIRE(k < L.openIndices.size(), "Every index on the LHS must appear somewhere on the RHS, here: " << I);
+        XERUS_REQUIRE(!used[k], "Traces and fixed indices are not allowed in the target of evaluation.");
+        XERUS_REQUIRE(L.openIndices[k].span == I.span, "The indexSpans in the target and base of evaluation must coincide.");
+        used[k] = 1;
+        for (size_t q = 0; q < I.span; ++q) slotOf[firstSlot[k] + q] = pos++;
+    }
+    for (size_t k = 0; k < used.size(); ++k)
+        XERUS_REQUIRE(used[k], "All indices of evalutation base must either be fixed, appear in the target or be part of a trace. Missing: "
+                                   << L.openIndices[k]);
+    return slotOf;
+}
+
+TensorNetwork product_network(const IndexedProduct& _p, const std::vector<Index>& _out) {
+    XERUS_REQUIRE(!_p.terms.empty(), "empty product");
+    Lowered L = lower(_p);
+    const std::vector<size_t> slotOf = output_slots(L, _out);
+    TensorNetwork& net = L.net;
+    net.require_valid_network();
+    // components without an external mode contract to one scalar, folded with the product's factor into a node
+    const value_t scalar = contract_unconnected(net) * _p.scale;
+    const size_t E = net.degree();
+    std::vector<TensorNetwork::Link> ext(E);
+    std::vector<size_t> dims(E);
+    for (size_t s = 0; s < E; ++s) {
+        ext[slotOf[s]] = net.externalLinks[s];
+        dims[slotOf[s]] = net.dimensions[s];
+    }
+    for (TensorNetwork::TensorNode& node : net.nodes)
+        for (TensorNetwork::Link& l : node.neighbors)
+            if (l.external) l.indexPosition = slotOf[l.indexPosition];
+    net.externalLinks = std::move(ext);
+    net.dimensions = std::move(dims);
+    if (scalar != 1.0) {
+        for (TensorNetwork::TensorNode& node : net.nodes)
+            if (!node.erased && node.tensorObject) {
+                node.tensorObject->factor *= scalar;
+                break;
+            }
+    }
+    net.require_valid_network();
+    return std::move(net);
+}
+
 Tensor evaluate_product(const IndexedProduct& _p, const std::vector<Index>& _out) {
     XERUS_REQUIRE(!_p.terms.empty(), "empty product");
     Lowered L = lower(_p);
@@ -243,32 +303,7 @@ Tensor evaluate_product(const IndexedProduct& _p, const std::vector<Index>& _out
     Tensor& R = *net.nodes[res].tensorObject;
 
     // output order (indexedTensorWritable.cpp:97-118)
-    const size_t E = net.degree();
-    const std::vector<Index> out = resolve(_out, E);
-    std::vector<size_t> slotOf(E);   // external slot -> output mode
-    {
-        std::vector<size_t> firstSlot(L.openIndices.size());
-        size_t s = 0;
-        for (size_t k = 0; k < L.openIndices.size(); ++k) {
-            firstSlot[k] = s;
-            s += L.openIndices[k].span;
-        }
-        std::vector<char> used(L.openIndices.size(), 0);
-        size_t pos = 0;
-        for (const Index& I : out) {
-            XERUS_REQUIRE(!I.fixed(), "Traces and fixed indices are not allowed in the target of evaluation.");
-            size_t k = 0;
-            while (k < L.openIndices.size() && L.openIndices[k] != I) ++k;
-            XERUS_REQUIRE(k < L.openIndices.size(), "Every index on the LHS must appear somewhere on the RHS, here: " << I);
-            XERUS_REQUIRE(!used[k], "Traces and fixed indices are not allowed in the target of evaluation.");
-            XERUS_REQUIRE(L.openIndices[k].span == I.span, "The indexSpans in the target and base of evaluation must coincide.");
-            used[k] = 1;
-            for (size_t q = 0; q < I.span; ++q) slotOf[firstSlot[k] + q] = pos++;
-        }
-        for (size_t k = 0; k < used.size(); ++k)
-            XERUS_REQUIRE(used[k], "All indices of evalutation base must either be fixed, appear in the target or be part of a trace. Missing: "
-                                       << L.openIndices[k]);
-    }
+    const std::vector<size_t> slotOf = output_slots(L, _out);
     std::vector<size_t> shuffle(R.degree());
     bool identity = true;
     for (size_t d = 0; d < R.degree(); ++d) {
@@ -408,5 +443,13 @@ IndexedSum operator+(IndexedSum _a, const IndexedTensor<Tensor>& _b) { return st
 IndexedSum operator-(IndexedSum _a, const IndexedTensor<Tensor>& _b) { return std::move(_a) - _b.as_product(); }
 
 value_t frob_norm(const IndexedTensor<Tensor>& _idxTensor) { return _idxTensor.tensorObject->frob_norm(); }
+
+// ---------------------------------------------------------------------------------------------- networks
+IndexedNetwork& IndexedNetwork::operator=(const IndexedProduct& _rhs) {
+    *network = internal::product_network(_rhs, indices);
+    return *this;
+}
+
+IndexedNetwork& IndexedNetwork::operator=(const IndexedTensor<Tensor>& _rhs) { return *this = _rhs.as_product(); }
 
 }  // namespace xerus

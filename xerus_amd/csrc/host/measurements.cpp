@@ -127,6 +127,13 @@ SinglePointMeasurementSet SinglePointMeasurementSet::random(const size_t _numMea
     return result;
 }
 
+SinglePointMeasurementSet SinglePointMeasurementSet::random(const size_t _numMeasurements, const TensorNetwork& _solution) {
+    SinglePointMeasurementSet result;
+    result.create_random_positions(_numMeasurements, _solution.dimensions);
+    result.measure(_solution);
+    return result;
+}
+
 SinglePointMeasurementSet SinglePointMeasurementSet::random(const size_t _numMeasurements, const std::vector<size_t>& _dimensions,
                                                             std::function<value_t(const std::vector<size_t>&)> _callback) {
     SinglePointMeasurementSet result;
@@ -188,11 +195,27 @@ void SinglePointMeasurementSet::measure(const TTTensor& _solution) {
     measuredValues = internal::evaluate_tt(_solution, dm);
 }
 
+void SinglePointMeasurementSet::measure(const TensorNetwork& _solution) {
+    XERUS_REQUIRE(_solution.degree() == degree(), "Degrees of solution and measurements must match!");
+    for (size_t i = 0; i < size(); ++i) measuredValues[i] = _solution[positions[i]];
+}
+
 void SinglePointMeasurementSet::measure(std::function<value_t(const std::vector<size_t>&)> _callback) {
     for (size_t i = 0; i < size(); ++i) measuredValues[i] = _callback(positions[i]);
 }
 
 double SinglePointMeasurementSet::test(const Tensor& _solution) const {
+    double error = 0.0, norm = 0.0;
+    for (size_t i = 0; i < size(); ++i) {
+        const double e = measuredValues[i] - _solution[positions[i]];
+        error += e * e;
+        norm += measuredValues[i] * measuredValues[i];
+    }
+    return std::sqrt(error / norm);
+}
+
+double SinglePointMeasurementSet::test(const TensorNetwork& _solution) const {
+    XERUS_REQUIRE(_solution.degree() == degree(), "Degrees of solution and measurements must match!");
     double error = 0.0, norm = 0.0;
     for (size_t i = 0; i < size(); ++i) {
         const double e = measuredValues[i] - _solution[positions[i]];

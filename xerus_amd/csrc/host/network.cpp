@@ -505,6 +505,55 @@ Tensor TensorNetwork::to_tensor() const {
 
 value_t TensorNetwork::frob_norm() const { return to_tensor().frob_norm(); }
 
+value_t TensorNetwork::operator[](const size_t _position) const {
+    require_valid_network();
+    if (degree() == 0) {
+        XERUS_REQUIRE(_position == 0, "Tried to access non-existing entry of TN");
+        value_t value = 1.0;
+        for (const TensorNode& node : nodes)
+            if (!node.erased) value *= (*node.tensorObject)[0];
+        return value;
+    }
+    std::vector<size_t> positions(degree());
+    size_t remains = _position;
+    for (size_t i = degree(); i > 1; --i) {
+        positions[i - 1] = remains % dimensions[i - 1];
+        remains /= dimensions[i - 1];
+    }
+    positions[0] = remains;
+    return (*this)[positions];
+}
+
+value_t TensorNetwork::operator[](const std::vector<size_t>& _positions) const {
+    require_valid_network();
+    XERUS_REQUIRE(_positions.size() == degree(), "Wrong number of positions: " << _positions.size() << " for degree " << degree());
+    for (size_t i = 0; i < degree(); ++i)
+        XERUS_REQUIRE(_positions[i] < dimensions[i], "Position " << _positions[i] << " out of range in mode " << i);
+    // the reference's partial copy (tensorNetwork.cpp:331-370): fix every node's external modes (slices of the
+    // device tensors), drop the external links, renumber the internal ones, contract what remains
+    TensorNetwork partial{Structure{}};
+    partial.nodes = nodes;
+    for (TensorNode& node : partial.nodes) {
+        if (node.erased) continue;
+        size_t killed = 0;
+        for (size_t i = 0; i < node.neighbors.size(); ++i)
+            if (node.neighbors[i].external) {
+                node.tensorObject->fix_mode(i - killed, _positions[node.neighbors[i].indexPosition]);
+                ++killed;
+            }
+        node.neighbors.erase(std::remove_if(node.neighbors.begin(), node.neighbors.end(), [](const Link& _l) { return _l.external; }),
+                             node.neighbors.end());
+        for (size_t i = 0; i < node.neighbors.size(); ++i)
+            partial.nodes[node.neighbors[i].other].neighbors[node.neighbors[i].indexPosition].indexPosition = i;
+    }
+    std::set<size_t> all;
+    for (size_t i = 0; i < partial.nodes.size(); ++i)
+        if (!partial.nodes[i].erased) all.insert(i);
+    if (all.empty()) return 1.0;
+    const size_t res = partial.contract(all);
+    return (*partial.nodes[res].tensorObject)[0];
+}
+
 Tensor& Tensor::operator=(const TensorNetwork& _network) { return *this = _network.to_tensor(); }
 
 }  // namespace xerus

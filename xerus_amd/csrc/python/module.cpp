@@ -247,6 +247,13 @@ PYBIND11_MODULE(xerus, m) {
     m.def("save_to_file", [](const TTTensor& _t, const std::string& _f, bool _tsv) {
         misc::save_to_file(_t, _f, _tsv ? misc::FileFormat::TSV : misc::FileFormat::BINARY);
     }, py::arg("tt"), py::arg("filename"), py::arg("tsv") = false);
+    m.def("save_to_file", [](const TensorNetwork& _t, const std::string& _f, bool _tsv) {
+        misc::save_to_file(_t, _f, _tsv ? misc::FileFormat::TSV : misc::FileFormat::BINARY);
+    }, py::arg("network"), py::arg("filename"), py::arg("tsv") = false);
+    // misc::load_from_file<TensorNetwork> / <TTTensor> / <Tensor> (misc/fileIO.h:139-163): the stored type must match
+    m.def("load_network_from_file", &misc::load_network_from_file);
+    m.def("load_tt_from_file", &misc::load_tt_from_file);
+    m.def("load_tensor_from_file", &misc::load_tensor_from_file);
     // the object type is read from the file's header (Tensor, TTTensor; a TensorNetwork file loads as its
     // contracted Tensor)
     m.def("load_from_file", [](const std::string& _f) -> py::object {
@@ -258,15 +265,22 @@ PYBIND11_MODULE(xerus, m) {
     m.def("file_type", &misc::file_type);
 
     // ------------------------------------------------------------------ TensorNetwork (results of chop)
+    py::class_<IndexedNetwork>(m, "IndexedNetwork")
+        .def("__lshift__", [](IndexedNetwork& _l, const IndexedProduct& _r) { _l = _r; })
+        .def("__lshift__", [](IndexedNetwork& _l, const IndexedTensor<Tensor>& _r) { _l = _r; });
     py::class_<TensorNetwork>(m, "TensorNetwork")
         .def(py::init<>())
         .def(py::init<Tensor>())
+        .def(py::init<const TensorNetwork&>())
         .def_readonly("dimensions", &TensorNetwork::dimensions)
         .def("degree", &TensorNetwork::degree)
         .def("num_nodes", &TensorNetwork::num_nodes)
         .def("frob_norm", &TensorNetwork::frob_norm)
         .def("to_tensor", &TensorNetwork::to_tensor)
-        .def("require_valid_network", &TensorNetwork::require_valid_network);
+        .def("require_valid_network", &TensorNetwork::require_valid_network)
+        .def("__call__", [](TensorNetwork& _t, py::args _a) { return _t(to_indices(_a)); }, py::keep_alive<0, 1>())
+        .def("__getitem__", [](const TensorNetwork& _t, size_t _i) { return _t[_i]; })
+        .def("__getitem__", [](const TensorNetwork& _t, const std::vector<size_t>& _i) { return _t[_i]; });
 
     // ------------------------------------------------------------------ TTTensor
     py::class_<IndexedTTStack>(m, "IndexedTTStack")
@@ -386,9 +400,11 @@ PYBIND11_MODULE(xerus, m) {
         .def("sort", &SinglePointMeasurementSet::sort, py::arg("positionsOnly") = false)
         .def("measure", py::overload_cast<const Tensor&>(&SinglePointMeasurementSet::measure))
         .def("measure", py::overload_cast<const TTTensor&>(&SinglePointMeasurementSet::measure))
+        .def("measure", py::overload_cast<const TensorNetwork&>(&SinglePointMeasurementSet::measure))
         .def("measure", py::overload_cast<std::function<value_t(const std::vector<size_t>&)>>(&SinglePointMeasurementSet::measure))
         .def("test", py::overload_cast<const Tensor&>(&SinglePointMeasurementSet::test, py::const_))
-        .def("test", py::overload_cast<const TTTensor&>(&SinglePointMeasurementSet::test, py::const_));
+        .def("test", py::overload_cast<const TTTensor&>(&SinglePointMeasurementSet::test, py::const_))
+        .def("test", py::overload_cast<const TensorNetwork&>(&SinglePointMeasurementSet::test, py::const_));
     py::class_<RankOneMeasurementSet>(m, "RankOneMeasurementSet")
         .def(py::init<>())
         .def(py::init<const RankOneMeasurementSet&>())

@@ -248,7 +248,6 @@ static void qr_solve_big(xrs_handle_t h, double* X, const double* A, size_t m, s
     }
 }
 
-// x = V S^+ U^T b, singular values <= EPSILON sigma_0 dropped (dgelsd with rcond = xerus::EPSILON, :704)
 // Pseudo-inverse solution X = V S^+ U^T B (singular values below 8 eps sigma_0 cut, dgelsd's rule) plus two
 // steps of iterative refinement x <- x - A^+ (A x - b) reusing the factors: the reference's dgesv / dsysv /
 // dgelsd residuals on ill-conditioned systems (fullTensor_solve.cxx "solve vs least squares", kappa ~ 1e6:

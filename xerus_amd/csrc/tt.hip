@@ -691,7 +691,7 @@ void chain_pass(TT& t, bool certify, ChainPass& out, int* host_status) {
     for (size_t k = 1; k < d; ++k) {       // left factors: Z_k (r_k x r_k) times the r_k x (n_k r_{k+1}) unfolding
         const size_t a = t.r[k], cols = t.cols_right(k);
         left.push_back({a, cols, a, a, cols, false, false, Z[k].d(), k + 1 < d ? W[k].d() : t.core[k], out.C[k]});
-        left.back().tri = (a <= 256 && true) ? kTriA : 0;
+        left.back().tri = a <= 256 ? kTriA : 0;
     }
     gemm_grouped(h, right);
     gemm_grouped(h, left);
