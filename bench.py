@@ -32,6 +32,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # gfx950 dense fp64 matrix peak (MI355X spec)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # gfx950 dense fp32 matrix peak (v_mfma_f32_*_f32, MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0           # HBM3E spec peak (MI355X_MICROARCH.md; 6.29 TB/s measured for a float4 copy)
 SEED = 0xBAADF00D               # src/xerus/test/test.cpp:105
 
@@ -185,6 +186,26 @@ def bench_cfg2(h):
     return {"workload": "A(i,j) = B(i,k) * C(k,j), 1024^3, fp64 MFMA GEMM", "us": round(ev["us_per_launch"], 2),
             "tflops": round(tf, 2), "frac_fp64_peak": round(tf / FP64_MFMA_PEAK_TFLOPS, 3),
             "timing": "dispatch begin/end events (hipExtLaunchKernelGGL), mean of 20"}
+
+
+def bench_cfg2_f32(h):
+    """BASELINE configs[1] on the fp32 matrix cores (xrs_gemm_f32, "MFMA fp32"): 1024^3, fp32 operands resident in
+    HBM; its error against the fp64 product of the same fp32 inputs."""
+    from xerus_amd import capi
+
+    n = 1024
+    rng = np.random.default_rng(1)
+    A32, B32 = rng.standard_normal((n, n)).astype(np.float32), rng.standard_normal((n, n)).astype(np.float32)
+    A, B, C = h.array_f32(A32), h.array_f32(B32), capi.Float32Array(h, (n, n))
+    ev = _events(h, capi.KFAM_GEMM, lambda: h.gemm_f32(C, n, n, 1.0, A, n, False, n, B, n, False), 50)
+    expect = A32.astype(np.float64) @ B32.astype(np.float64)
+    err = float(np.linalg.norm(C.numpy() - expect) / np.linalg.norm(expect))
+    for d in (A, B, C):
+        d.free()
+    tf = 2.0 * n ** 3 / (ev["us_per_launch"] * 1e-6) / 1e12
+    return {"workload": "A(i,j) = B(i,k) * C(k,j), 1024^3, fp32 MFMA GEMM (xrs_gemm_f32)", "us": round(ev["us_per_launch"], 2),
+            "tflops": round(tf, 2), "frac_fp32_peak": round(tf / FP32_MFMA_PEAK_TFLOPS, 3), "peak_tflops": FP32_MFMA_PEAK_TFLOPS,
+            "rel_frob_err_vs_fp64": err, "timing": "dispatch begin/end events (hipExtLaunchKernelGGL), mean of 50"}
 
 
 def bench_cfg1(xe):
@@ -473,9 +494,18 @@ def main():
     for _ in range(args.steps):
         x.dot_f32(y)
     t32 = (time.perf_counter() - t32) / args.steps
+    # accuracy: the step's independent x, y (|<x,y>| ~ 2e-7 ||x|| ||y||: error relative to the norms and to the value)
+    # and the correlated pair <x,x> (relative to the value)
+    nxy = x.frob_norm() * y.frob_norm()
+    xx64, xx32 = x.dot(x), x.dot_f32(x)
     dot_f32 = {"ms": round(t32 * 1e3, 4), "tflops": round(f_dot / t32 / 1e12, 3),
-               "rel_err": abs(d32 - d64) / (x.frob_norm() * y.frob_norm()),
-               "path": "xrs_tt_dot_f32: two-ended zipper, v_mfma_f32_16x16x4_f32, fp64 cores rounded at load"}
+               "frac_fp32_peak": round(f_dot / t32 / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+               "rel_err": abs(d32 - d64) / nxy, "rel_err_norms": abs(d32 - d64) / nxy,
+               "rel_err_value": abs(d32 - d64) / abs(d64), "value_over_norms": abs(d64) / nxy,
+               "xx_rel_err_value": abs(xx32 - xx64) / abs(xx64),
+               "timing": "host wall per call (synchronous: includes the read-back and host exponent sum)",
+               "path": "xrs_tt_dot_f32: two-ended zipper of xrs_gemm_f32-family launches (v_mfma_f32_16x16x4_f32), fp64 cores "
+                       "rounded at load, power-of-two normalised T and environments"}
 
     # Roofline passes: the same K steps again with a HIP event pair on every GEMM launch (the start / stop
     # events of hipExtLaunchKernelGGL on the stream each launch goes to: the dispatch's own begin / end
@@ -517,7 +547,8 @@ def main():
 
     extras = {}
     if world == 1 and not args.no_extras:
-        for key, fn in [("cfg1", lambda: bench_cfg1(xe)), ("cfg2", lambda: bench_cfg2(h)), ("cfg3", lambda: bench_cfg3(h, xe)),
+        for key, fn in [("cfg1", lambda: bench_cfg1(xe)), ("cfg2", lambda: bench_cfg2(h)), ("cfg2_f32", lambda: bench_cfg2_f32(h)),
+                        ("cfg3", lambda: bench_cfg3(h, xe)),
                         ("cfg4", lambda: bench_cfg4(h, xe)), ("permute", lambda: bench_permute(h)), ("svd", lambda: bench_svd(h))]:
             try:
                 extras[key] = fn()

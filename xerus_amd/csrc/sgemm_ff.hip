@@ -21,3 +21,10 @@ extern "C" int xrs_gemm_f32(xrs_handle_t h, float* C, size_t M, size_t N, float 
         xrs::sgemm<float, float>(h, C, M, N, alpha, A, lda, transA != 0, K, B, ldb, transB != 0);
     });
 }
+
+#ifdef XRS_SG_STAMPS
+extern "C" int xrs_debug_sg_stamps(void* buf) {
+    unsigned long long* q = static_cast<unsigned long long*>(buf);
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sg_stamps), &q, sizeof(q)) == hipSuccess ? 0 : 1;
+}
+#endif

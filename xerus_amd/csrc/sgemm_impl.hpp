@@ -24,10 +24,10 @@
 //      row-contiguous staging writes (16 or 8 B per lane along r) keep every vector whole and aligned.
 //  - MFMA k order: within a 16-deep chunk, lane group g = lane >> 4 of MFMA j takes k = 4 g + j (A and B
 //    alike), so a lane's four k of one chunk are one ds_read offset pattern.
-//  - Split-K (grid.z) for grids that cannot fill 256 CUs: the slices store fp32 slabs write-through (sc1),
-//    draw an arrival ticket, and the last slice of a tile sums all slabs in slice order (deterministic),
-//    applies alpha and writes C (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores, agent-scope ticket,
-//    sc1 loads); tile grids beyond the ticket array use a separate fixed-order reduce kernel.
+//  - Split-K (grid.z) for grids that cannot fill 256 CUs: the slices store their partial tiles in the
+//    accumulator layout with 16-B write-through (sc1) buffer stores, draw an arrival ticket, and the last slice
+//    of a tile sums all slabs in a fixed order with 16-B sc1 loads (deterministic), applies alpha and writes C
+//    (MI355X_MICROARCH.md, hand-off table row 1: sc1 stores, agent-scope ticket, sc1 loads).
 //  - Optional max|C| (atomicMax on the float bits) and power-of-two operand scales from such words, and
 //    per-workgroup max|.| slots of fp64 operands: the fp32 TT zipper's range control (dot32.hip, sgemm.hpp).
 #pragma once
@@ -40,6 +40,23 @@
 #include <hip/hip_ext.h>
 
 #include "sgemm.hpp"
+
+#ifdef XRS_SG_STAMPS
+// Diagnostic build only (tools/sgemm_stamps.py): thread 0 of every workgroup writes s_memtime at the kernel's
+// phase boundaries to g_sg_stamps[8 wg + i]: 0 start, 1 prologue done, 2 main loop done, 3 epilogue / ticket
+// done, 4 end (the last slice: after the combine); [7] = XCC id << 32 | HW id.
+__device__ unsigned long long* g_sg_stamps = nullptr;
+#define XRS_SG_STAMP(i)                                                                                      \
+    if (threadIdx.x == 0 && g_sg_stamps != nullptr) {                                                       \
+        const size_t wg_ = blockIdx.x + size_t(gridDim.x) * blockIdx.z;                                     \
+        g_sg_stamps[8 * wg_ + (i)] = __builtin_amdgcn_s_memtime();                                          \
+        if ((i) == 0)                                                                                        \
+            g_sg_stamps[8 * wg_ + 7] = (static_cast<unsigned long long>(__builtin_amdgcn_s_getreg((31 << 11) | 20)) << 32) | \
+                                       __builtin_amdgcn_s_getreg((31 << 11) | 4);                            \
+    }
+#else
+#define XRS_SG_STAMP(i)
+#endif
 
 namespace xrs {
 namespace sg {
@@ -190,6 +207,7 @@ struct Args {
     unsigned* cmax_a;   // per-workgroup max|A| / max|B| slots of fp64 operands (kCmaxSlots words each)
     unsigned* cmax_b;
     float* slab;
+    unsigned slab_bytes;
     int* tickets;
     int tiles_m;
     int xcd;   // 1: tiles sharing a B column panel on one XCD, 2: sharing an A row panel, 0: column-major
@@ -231,10 +249,11 @@ __device__ __forceinline__ void block_max_atomic(unsigned* w, float m, float* re
     }
 }
 
-// Main loop: step t computes LDS buffer t % 2, then writes step t+1 (register slot (t+1) % 2) into the other
-// buffer and issues the loads of step t+2; one barrier per step. (A 3-stage LDS ring whose last chunk read
+// Main loop: step t computes LDS buffer t % 2, then writes step t+1 (register slot (t+1) % PD) into the other
+// buffer and issues the loads of step t+PD into slot t % PD; one barrier per step. PD = 4 keeps twice the
+// bytes in flight of PD = 2: short-K slices (the environment products' 10 steps) are load-latency bound. (A 3-stage LDS ring whose last chunk read
 // the next step's first fragments ahead of the barrier measured slower on every shape: DESIGN.md §3.6.)
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK, bool STAG, bool TA, bool TB, class EA, class EB, int MODE>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, bool TA, bool TB, class EA, class EB, int MODE>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
     constexpr int ST = 2;
     constexpr bool VEC = MODE >= 1, WHOLE = MODE == 2;
@@ -273,6 +292,7 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
             tn = b / p.tiles_m;
         }
     }
+    XRS_SG_STAMP(0)
     const int m0 = tm * BM, n0 = tn * BN;
     const int kbeg = int(blockIdx.z) * p.kps, kend = min(p.K, kbeg + p.kps);
     const int nsteps = (kend - kbeg + BK - 1) / BK;   // >= 1: the host launches non-empty slices only
@@ -287,14 +307,16 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    SA ra[2];
-    SB rb[2];
+    static_assert(PD == 2 || PD == 4, "register ring of 2 or 4 K-steps");
+    SA ra[PD];
+    SB rb[PD];
     EA vmax_a = 0;
     EB vmax_b = 0;
-    ra[0].template init<IA>(p.lda);
-    ra[1].template init<IA>(p.lda);
-    rb[0].template init<IB>(p.ldb);
-    rb[1].template init<IB>(p.ldb);
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+        ra[u].template init<IA>(p.lda);
+        rb[u].template init<IB>(p.ldb);
+    }
     auto load = [&](auto slot_c, int t) {
         constexpr int s = decltype(slot_c)::value;
         if constexpr (WHOLE) t = min(t, nsteps - 1);   // (the ring's loads past the slice re-read its last step)
@@ -349,44 +371,43 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
     using I1 = std::integral_constant<int, 1>;
 
     {
-        // ring: register slot / LDS buffer s holds K-step t with t % 2 == s
-        load(I0{}, 0);
-        load(I1{}, 1);
+        // ring: register slot t % PD holds K-step t (its loads issued PD steps ahead), LDS buffer t % 2
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            (load(std::integral_constant<int, U>{}, U), ...);
+        }(std::make_integer_sequence<int, PD>{});
         store(I0{}, 0, 0);
         __syncthreads();
-        int t = 0;
-        // STAG: the second half of the waves (wave >= NW/2: each SIMD holds one wave of either half) stage step
-        // t+1 BEFORE computing step t (buffer (t+1) % 2 is free once the barrier ending step t-1 has passed),
-        // so on every SIMD one wave's MFMAs run beside the other wave's staging loads, conversions and LDS
-        // writes instead of both waves alternating between the two in lockstep
-        const bool late = STAG && wave >= (NT / 64) / 2;
-        if (late) {
-            for (; t + 2 <= nsteps; t += 2) {
-                store(I1{}, 1, t + 1);
-                load(I0{}, t + 2);
-                compute(0);
-                __syncthreads();
-                store(I0{}, 0, t + 2);
-                load(I1{}, t + 3);
-                compute(1);
-                __syncthreads();
-            }
-        } else {
-            for (; t + 2 <= nsteps; t += 2) {
-                // (steps past the slice end load clamped addresses and store into the idle buffer: no branch)
-                compute(0);
-                store(I1{}, 1, t + 1);
-                load(I0{}, t + 2);
-                __syncthreads();
-                compute(1);
-                store(I0{}, 0, t + 2);
-                load(I1{}, t + 3);
-                __syncthreads();
-            }
+        XRS_SG_STAMP(1)
+        int t0 = 0;
+        // steady state, no guards: the loads of steps past the slice re-read valid addresses and their stores
+        // go to the idle buffer
+        for (; t0 + PD <= nsteps; t0 += PD) {
+            [&]<int... U>(std::integer_sequence<int, U...>) {
+                (([&] {
+                     const int t = t0 + U;
+                     compute(U & 1);
+                     store(std::integral_constant<int, (U + 1) % PD>{}, (U + 1) & 1, t + 1);
+                     load(std::integral_constant<int, U>{}, t + PD);
+                     __syncthreads();
+                 }()),
+                 ...);
+            }(std::make_integer_sequence<int, PD>{});
         }
-        if (t < nsteps) compute(0);
+        // tail: fewer than PD steps left (no loads: they were issued by the steady state or the prologue)
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            (([&] {
+                 const int t = t0 + U;
+                 if (t < nsteps) {
+                     compute(U & 1);
+                     if (t + 1 < nsteps) store(std::integral_constant<int, (U + 1) % PD>{}, (U + 1) & 1, t + 1);
+                     __syncthreads();
+                 }
+             }()),
+             ...);
+        }(std::make_integer_sequence<int, PD>{});
     }
 
+    XRS_SG_STAMP(2)
     // max|.| of the fp64 operands into this workgroup's slot (no single hot word: kCmaxSlots slots per launch)
     {
         const unsigned slot = (blockIdx.x + gridDim.x * blockIdx.z) % unsigned(kCmaxSlots);
@@ -445,30 +466,24 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
             __syncthreads();   // (the K-group reduction above read the LDS)
             block_max_atomic(p.amax, mx, lds);
         }
+        XRS_SG_STAMP(3)
         return;
     }
-    // ---- split-K: this slice's slab
-    const size_t MN = size_t(M) * size_t(N);
-    float* slab = p.slab + size_t(blockIdx.z) * MN;
+    // ---- split-K: this slice's partial tile in the accumulator layout -- the float4 of block (i, j) of lane l
+    // of the wave at position pos at ((pos TM + i) TN + j) 64 + l, so one wave instruction writes 1 KB
+    // contiguously -- at slab + (z tiles + x) BM BN for slice z of tile x; 16-B write-through (sc1) buffer
+    // stores, drained before the ticket (MI355X_MICROARCH.md, hand-off table row 1)
+    static_assert(WGM * WGN * TM * TN * 256 == BM * BN, "accumulator layout covers the tile");
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, int(p.slab_bytes), 0x00020000);
+    auto soff = [&](int z, int i, int j) {
+        return int(((size_t(z) * gridDim.x + blockIdx.x) * (BM * BN) + size_t(((pos * TM + i) * TN + j) * 64 + lane) * 4) * 4);
+    };
     if (kg == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int col = n0 + wn + 16 * j + lc;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m0 + wm + 16 * i + 4 * lq + r;
-                    if (row < M && col < N) {
-                        if (p.tickets != nullptr)   // write-through (sc1): visible to the last slice on any XCD
-                            __hip_atomic_store(&slab[size_t(row) * N + col], acc[i][j][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        else
-                            slab[size_t(row) * N + col] = acc[i][j][r];
-                    }
-                }
-            }
+            for (int j = 0; j < TN; ++j) __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rs, soff(blockIdx.z, i, j), 0, 16);
     }
-    if (p.tickets == nullptr) return;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float* flag = lds;   // the one LDS array (no second __shared__ object)
@@ -479,75 +494,107 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
         flag[0] = last ? 1.0f : 0.0f;
     }
     __syncthreads();
+    XRS_SG_STAMP(3)
     if (flag[0] == 0.0f) return;
-    // last slice: every thread of the workgroup sums a share of the tile over all slabs in slice order
-    // (sc1 loads, 8 slabs in flight per element before their adds)
+    __syncthreads();   // (every thread has read the flag before the LDS is reused below)
+    // last slice: wave group g sums the slabs z = g, g + WGK, ... in slice order (16-B sc1 loads, U slabs per
+    // round trip), then the groups' sums are added in group order through the LDS: a fixed order, so the
+    // result is the same bits whichever slice arrives last
     const int S = int(gridDim.z);
-    float mx = 0.0f;
-    for (int e = tid; e < BM * BN; e += NT) {
-        const int row = m0 + e / BN, col = n0 + e % BN;
-        if (row >= M || col >= N) continue;
-        const size_t o = size_t(row) * N + col;
-        float s = 0.0f;
-        for (int z0 = 0; z0 < S; z0 += 8) {
-            float v[8];
+    constexpr int U = (32 / (TM * TN)) < 1 ? 1 : ((32 / (TM * TN)) > 8 ? 8 : (32 / (TM * TN)));
+    f4 sum[TM][TN];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                v[u] = (z0 + u < S) ? __hip_atomic_load(&p.slab[size_t(z0 + u) * MN + o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (z0 + u < S) s += v[u];
+        for (int j = 0; j < TN; ++j) sum[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int z0 = kg; z0 < S; z0 += U * WGK) {
+        f4 v[U][TM][TN];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int z = min(z0 + u * WGK, S - 1);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) v[u][i][j] = __builtin_amdgcn_raw_buffer_load_b128(rs, soff(z, i, j), 0, 16);
         }
-        const float out = p.alpha * s;
-        p.C[o] = out;
-        mx = fmaxf(mx, fabsf(out));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float keep = (z0 + u * WGK < S) ? 1.0f : 0.0f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) sum[i][j] += keep * v[u][i][j];
+        }
+    }
+    if constexpr (WGK > 1) {
+        float* red = lds;
+        if (kg > 0) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        red[((((kg - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane] = sum[i][j][r];
+        }
+        __syncthreads();
+        if (kg == 0)
+#pragma unroll
+            for (int g = 1; g < WGK; ++g)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            sum[i][j][r] += red[((((g - 1) * (WGM * WGN) + pos) * TM * TN + i * TN + j) * 4 + r) * 64 + lane];
+    }
+    float mx = 0.0f;
+    if (kg == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int col = n0 + wn + 16 * j + lc;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m0 + wm + 16 * i + 4 * lq + r;
+                    if (row < M && col < N) {
+                        const float v = p.alpha * sum[i][j][r];
+                        p.C[size_t(row) * N + col] = v;
+                        mx = fmaxf(mx, fabsf(v));
+                    }
+                }
+            }
     }
     if (p.amax != nullptr) {
-        __syncthreads();   // (flag[0] was read from the LDS above)
+        __syncthreads();   // (the group reduction read the LDS)
         block_max_atomic(p.amax, mx, lds);
     }
-}
-
-// fixed-order split-K reduce (tile grids beyond the ticket array): C = alpha sum_z slab[z], max|C|
-__global__ void __launch_bounds__(256) k_sslab_reduce(const float* __restrict__ slab, int S, size_t MN, float* __restrict__ C,
-                                                     float alpha, unsigned* __restrict__ amax) {
-    float mx = 0.0f;
-    for (size_t i = size_t(blockIdx.x) * 256 + threadIdx.x; i < MN; i += size_t(gridDim.x) * 256) {
-        float s = 0.0f;
-        for (int z0 = 0; z0 < S; z0 += 8) {
-            float v[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) v[u] = (z0 + u < S) ? __builtin_nontemporal_load(&slab[size_t(z0 + u) * MN + i]) : 0.0f;
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (z0 + u < S) s += v[u];
-        }
-        C[i] = alpha * s;
-        mx = fmaxf(mx, fabsf(alpha * s));
-    }
-    __shared__ float red[4];
-    if (amax != nullptr) block_max_atomic(amax, mx, red);
+    XRS_SG_STAMP(4)
 }
 
 // ------------------------------------------------------------------------------------------- host side
 struct Cfg {
     int bm, bn, bk;
 };
-// production tiles: 0: 128x128 (8 waves 2x4, wave 64x32)   1: 64x64 (8 waves 2x2x2: wave 32x32, K-chunks over 2
-// groups)   2: 64x80 (8 waves 4x1x2, wave 16x80)   3: 80x64 (8 waves 1x4x2, wave 80x16)   4: 32x32 (2 waves, wave
-// 16x32). 5-9: loop forms measured against them (profiles/r05/sgemm_probe_*.txt), for A/B runs only (XRS_SGEMM,
-// fp32 operands): 5 64x64 with 64-deep K-steps, 6 64x64 staggered, 7 64x80 staggered, 8 128x128 staggered,
-// 9 80x64 staggered
-constexpr int kNumCfgs = 10;
+// production tiles: 0: 128x128 (8 waves 2x4, wave 64x32, 2-step ring)   1: 64x64 (8 waves 2x2x2: wave 32x32, K-chunks
+// over 2 groups)   2: 64x80 (8 waves 4x1x2, wave 16x80)   3: 80x64 (8 waves 1x4x2, wave 80x16)   4: 32x32 (2 waves, wave
+// 16x32, 2-step ring); 1-3 with a 4-step register ring. 5-9: forms measured against them (profiles/r05/), for A/B runs
+// only (XRS_SGEMM, fp32 operands): 5 64x64 with 64-deep K-steps, 6 / 7 / 9 the 64x64 / 64x80 / 80x64 tiles with a
+// 2-step ring, 8 128x128 with a 4-step ring, 10 64x64 with 16 waves (4 K-groups, 64-deep steps), 11 / 12 32x80 /
+// 80x32 with 4 waves (two workgroups per CU on the TT products' grids)
+constexpr int kNumCfgs = 13;
 constexpr Cfg kCfgs[kNumCfgs] = {{128, 128, 32}, {64, 64, 32}, {64, 80, 32}, {80, 64, 32}, {32, 32, 32},
-                                 {64, 64, 64},   {64, 64, 32}, {64, 80, 32}, {128, 128, 32}, {80, 64, 32}};
+                                 {64, 64, 64},   {64, 64, 32}, {64, 80, 32}, {128, 128, 32}, {80, 64, 32},
+                                 {64, 64, 64},   {32, 80, 32}, {80, 32, 32}};
 
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK, bool STAG, class EA, class EB>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, class EA, class EB>
 void launch_cfg(xrs_handle_t h, const Args& p, bool ta, bool tb, int mode, int tiles, int splits, double bytes) {
     const dim3 grid(unsigned(tiles), 1u, unsigned(splits));
     KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(p.M) * double(p.N) * double(p.K), bytes, true);
 #define XRS_SG(TA_, TB_, MODE_)                                                                                    \
-    hipExtLaunchKernelGGL((k_sgemm<BM, BN, WGM, WGN, WGK, BK, STAG, TA_, TB_, EA, EB, MODE_>), grid, dim3(WGM * WGN * WGK * 64), \
+    hipExtLaunchKernelGGL((k_sgemm<BM, BN, WGM, WGN, WGK, BK, PD, TA_, TB_, EA, EB, MODE_>), grid, dim3(WGM * WGN * WGK * 64), \
                           0, h->stream, timer.start(), timer.stop(), 0, p)
 #define XRS_SG_FLAGS(MODE_)                                  \
     if (!ta && !tb) XRS_SG(false, false, MODE_);              \
@@ -622,41 +669,38 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
         if (double(N) >= double(M)) xg = (tn % 8 == 0) ? 1 : 0;
         else xg = (tm % 8 == 0) ? 2 : 0;
     }
+    // split-K slabs: one accumulator-layout tile per slice and tile (the in-launch combine reads them)
     DevBuf slab;
-    if (splits > 1) slab = DevBuf(h, size_t(splits) * Ms * Ns * sizeof(float));
-    const char* ce = std::getenv("XRS_SGEMM_COMBINE");
-    const bool g_no_combine = ce != nullptr && ce[0] == '0';
-    int* tickets = (splits > 1 && tiles <= xrs_handle_s::kTicketCap && !g_no_combine) ? h->tickets : nullptr;
+    const size_t slab_bytes = splits > 1 ? size_t(splits) * size_t(tiles) * size_t(bm) * size_t(bn) * sizeof(float) : 0;
+    XRS_REQUIRE(slab_bytes < (size_t(1) << 31), "split-K slabs exceed 2 GiB");
+    XRS_REQUIRE(splits == 1 || tiles <= xrs_handle_s::kTicketCap, "split-K tile grid exceeds the ticket array");
+    if (splits > 1) slab = DevBuf(h, slab_bytes);
     Args p{A, lda, B, ldb, C, M, N, K, kps, alpha, x.sa, x.sb, x.amax, x.cmax_a, x.cmax_b, splits > 1 ? slab.as<float>() : nullptr,
-           tickets, (M + kCfgs[cfg].bm - 1) / kCfgs[cfg].bm, xg};
+           unsigned(slab_bytes), splits > 1 ? h->tickets : nullptr, (M + kCfgs[cfg].bm - 1) / kCfgs[cfg].bm, xg};
     const double bytes = double(sizeof(EA)) * M * K + double(sizeof(EB)) * K * N + 4.0 * M * N * (splits > 1 ? 2 * splits : 1);
 #define XRS_CFG(...) launch_cfg<__VA_ARGS__, EA, EB>(h, p, ta, tb, mode, tiles, splits, bytes)
     switch (cfg) {
-        case 0: XRS_CFG(128, 128, 2, 4, 1, 32, false); break;
-        case 1: XRS_CFG(64, 64, 2, 2, 2, 32, false); break;
-        case 2: XRS_CFG(64, 80, 4, 1, 2, 32, false); break;
-        case 3: XRS_CFG(80, 64, 1, 4, 2, 32, false); break;
-        case 4: XRS_CFG(32, 32, 2, 1, 1, 32, false); break;
+        case 0: XRS_CFG(128, 128, 2, 4, 1, 32, 2); break;
+        case 1: XRS_CFG(64, 64, 2, 2, 2, 32, 4); break;
+        case 2: XRS_CFG(64, 80, 4, 1, 2, 32, 4); break;
+        case 3: XRS_CFG(80, 64, 1, 4, 2, 32, 4); break;
+        case 4: XRS_CFG(32, 32, 2, 1, 1, 32, 2); break;
         default:
             if constexpr (kTune) {
                 switch (cfg) {
-                    case 5: XRS_CFG(64, 64, 2, 2, 2, 64, false); break;
-                    case 6: XRS_CFG(64, 64, 2, 2, 2, 32, true); break;
-                    case 7: XRS_CFG(64, 80, 4, 1, 2, 32, true); break;
-                    case 8: XRS_CFG(128, 128, 2, 4, 1, 32, true); break;
-                    default: XRS_CFG(80, 64, 1, 4, 2, 32, true); break;
+                    case 5: XRS_CFG(64, 64, 2, 2, 2, 64, 2); break;
+                    case 6: XRS_CFG(64, 64, 2, 2, 2, 32, 2); break;
+                    case 7: XRS_CFG(64, 80, 4, 1, 2, 32, 2); break;
+                    case 8: XRS_CFG(128, 128, 2, 4, 1, 32, 4); break;
+                    case 9: XRS_CFG(80, 64, 1, 4, 2, 32, 2); break;
+                    case 10: XRS_CFG(64, 64, 2, 2, 4, 64, 2); break;
+                    case 11: XRS_CFG(32, 80, 2, 1, 2, 32, 4); break;
+                    default: XRS_CFG(80, 32, 1, 2, 2, 32, 4); break;
                 }
             }
             break;
     }
 #undef XRS_CFG
-    if (splits > 1 && tickets == nullptr) {
-        const size_t MN = Ms * Ns;
-        const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 2048));
-        KernelTimer timer(h, XRS_KFAM_ELEMWISE, double(MN) * splits, 4.0 * double(MN) * (splits + 1));
-        hipLaunchKernelGGL(k_sslab_reduce, dim3(blocks), dim3(256), 0, h->stream, slab.as<float>(), splits, MN, C, alpha, x.amax);
-        check_launch("k_sslab_reduce");
-    }
 }
 
 }  // namespace xrs
