@@ -253,9 +253,9 @@ __device__ __forceinline__ void block_max_atomic(unsigned* w, float m, float* re
 // buffer and issues the loads of step t+PD into slot t % PD; one barrier per step. PD = 4 keeps twice the
 // bytes in flight of PD = 2: short-K slices (the environment products' 10 steps) are load-latency bound. (A 3-stage LDS ring whose last chunk read
 // the next step's first fragments ahead of the barrier measured slower on every shape: DESIGN.md §3.6.)
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, bool TA, bool TB, class EA, class EB, int MODE>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, int ST, bool TA, bool TB, class EA, class EB, int MODE>
 __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
-    constexpr int ST = 2;
+    static_assert(ST == 2 || ST == 3, "2 or 3 LDS stages");
     constexpr bool VEC = MODE >= 1, WHOLE = MODE == 2;
     // fp32-only products carry no operand scales (the fp32 zipper's mixed products always do)
     constexpr bool SC = !(std::is_same<EA, float>::value && std::is_same<EB, float>::value);
@@ -367,10 +367,67 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
              ...);
         }(std::make_integer_sequence<int, NQW>{});
     };
+    // ST = 3: chunk 0 of step t is already in fragment set S0 (read during step t-1); the last chunk's MFMAs
+    // run beside the reads of step t+1's chunk 0 from buffer `nbuf` (complete since the barrier that ended step
+    // t-1), so no barrier sits between a wave's fragment reads and its MFMAs
+    auto compute3 = [&](auto s0_c, int buf, int nbuf) {
+        constexpr int S0 = decltype(s0_c)::value;
+        [&]<int... Q>(std::integer_sequence<int, Q...>) {
+            (([&] {
+                 constexpr int cur = (S0 + Q) & 1, nxt = (S0 + Q + 1) & 1;
+                 if constexpr (Q + 1 < NQW) frag(std::integral_constant<int, nxt>{}, buf, Q + 1);
+                 else frag(std::integral_constant<int, nxt>{}, nbuf, 0);
+                 __builtin_amdgcn_sched_barrier(0);
+                 mfma(std::integral_constant<int, cur>{});
+             }()),
+             ...);
+        }(std::make_integer_sequence<int, NQW>{});
+    };
     using I0 = std::integral_constant<int, 0>;
     using I1 = std::integral_constant<int, 1>;
 
-    {
+    if constexpr (ST == 3) {
+        // register slot (t+2) % PD holds K-step t+2 at the start of step t (its loads issued PD steps before its
+        // store); LDS buffer t % 3 holds step t: step t writes step t+2 into buffer (t+2) % 3, last read in step
+        // t-1, before the barrier that ends it
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            (load(std::integral_constant<int, U>{}, U), ...);
+        }(std::make_integer_sequence<int, PD>{});
+        store(I0{}, 0, 0);
+        store(I1{}, 1, 1);
+        load(I0{}, PD);
+        load(I1{}, PD + 1);
+        __syncthreads();
+        XRS_SG_STAMP(1)
+        frag(I0{}, 0, 0);
+        int t0 = 0, b0 = 0;   // b0 = t0 % 3
+        for (; t0 + PD <= nsteps; t0 += PD) {
+            [&]<int... U>(std::integer_sequence<int, U...>) {
+                (([&] {
+                     const int t = t0 + U;
+                     const int bc = (b0 + U) % 3, bn = (b0 + U + 1) % 3, bs = (b0 + U + 2) % 3;
+                     compute3(std::integral_constant<int, (U * NQW) & 1>{}, bc, bn);
+                     store(std::integral_constant<int, (U + 2) % PD>{}, bs, t + 2);
+                     load(std::integral_constant<int, (U + 2) % PD>{}, t + 2 + PD);
+                     __syncthreads();
+                 }()),
+                 ...);
+            }(std::make_integer_sequence<int, PD>{});
+            b0 = (b0 + PD) % 3;
+        }
+        [&]<int... U>(std::integer_sequence<int, U...>) {
+            (([&] {
+                 const int t = t0 + U;
+                 if (t < nsteps) {
+                     const int bc = (b0 + U) % 3, bn = (b0 + U + 1) % 3, bs = (b0 + U + 2) % 3;
+                     compute3(std::integral_constant<int, (U * NQW) & 1>{}, bc, bn);
+                     if (t + 2 < nsteps) store(std::integral_constant<int, (U + 2) % PD>{}, bs, t + 2);
+                     __syncthreads();
+                 }
+             }()),
+             ...);
+        }(std::make_integer_sequence<int, PD>{});
+    } else {
         // ring: register slot t % PD holds K-step t (its loads issued PD steps ahead), LDS buffer t % 2
         [&]<int... U>(std::integer_sequence<int, U...>) {
             (load(std::integral_constant<int, U>{}, U), ...);
@@ -582,19 +639,19 @@ struct Cfg {
 // over 2 groups)   2: 64x80 (8 waves 4x1x2, wave 16x80)   3: 80x64 (8 waves 1x4x2, wave 80x16)   4: 32x32 (2 waves, wave
 // 16x32, 2-step ring); 1-3 with a 4-step register ring. 5-9: forms measured against them (profiles/r05/), for A/B runs
 // only (XRS_SGEMM, fp32 operands): 5 64x64 with 64-deep K-steps, 6 / 7 / 9 the 64x64 / 64x80 / 80x64 tiles with a
-// 2-step ring, 8 128x128 with a 4-step ring, 10 64x64 with 16 waves (4 K-groups, 64-deep steps), 11 / 12 32x80 /
-// 80x32 with 4 waves (two workgroups per CU on the TT products' grids)
+// 2-step ring, 8 128x128 with 3 LDS stages, 10 / 11 / 12 the 64x64 / 64x80 / 80x64 tiles with 3 LDS stages (the next
+// step's first fragments read ahead of the barrier)
 constexpr int kNumCfgs = 13;
 constexpr Cfg kCfgs[kNumCfgs] = {{128, 128, 32}, {64, 64, 32}, {64, 80, 32}, {80, 64, 32}, {32, 32, 32},
                                  {64, 64, 64},   {64, 64, 32}, {64, 80, 32}, {128, 128, 32}, {80, 64, 32},
-                                 {64, 64, 64},   {32, 80, 32}, {80, 32, 32}};
+                                 {64, 64, 32},   {64, 80, 32}, {80, 64, 32}};
 
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, class EA, class EB>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, int ST, class EA, class EB>
 void launch_cfg(xrs_handle_t h, const Args& p, bool ta, bool tb, int mode, int tiles, int splits, double bytes) {
     const dim3 grid(unsigned(tiles), 1u, unsigned(splits));
     KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(p.M) * double(p.N) * double(p.K), bytes, true);
 #define XRS_SG(TA_, TB_, MODE_)                                                                                    \
-    hipExtLaunchKernelGGL((k_sgemm<BM, BN, WGM, WGN, WGK, BK, PD, TA_, TB_, EA, EB, MODE_>), grid, dim3(WGM * WGN * WGK * 64), \
+    hipExtLaunchKernelGGL((k_sgemm<BM, BN, WGM, WGN, WGK, BK, PD, ST, TA_, TB_, EA, EB, MODE_>), grid, dim3(WGM * WGN * WGK * 64), \
                           0, h->stream, timer.start(), timer.stop(), 0, p)
 #define XRS_SG_FLAGS(MODE_)                                  \
     if (!ta && !tb) XRS_SG(false, false, MODE_);              \
@@ -680,22 +737,22 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
     const double bytes = double(sizeof(EA)) * M * K + double(sizeof(EB)) * K * N + 4.0 * M * N * (splits > 1 ? 2 * splits : 1);
 #define XRS_CFG(...) launch_cfg<__VA_ARGS__, EA, EB>(h, p, ta, tb, mode, tiles, splits, bytes)
     switch (cfg) {
-        case 0: XRS_CFG(128, 128, 2, 4, 1, 32, 2); break;
-        case 1: XRS_CFG(64, 64, 2, 2, 2, 32, 4); break;
-        case 2: XRS_CFG(64, 80, 4, 1, 2, 32, 4); break;
-        case 3: XRS_CFG(80, 64, 1, 4, 2, 32, 4); break;
-        case 4: XRS_CFG(32, 32, 2, 1, 1, 32, 2); break;
+        case 0: XRS_CFG(128, 128, 2, 4, 1, 32, 2, 2); break;
+        case 1: XRS_CFG(64, 64, 2, 2, 2, 32, 4, 2); break;
+        case 2: XRS_CFG(64, 80, 4, 1, 2, 32, 4, 2); break;
+        case 3: XRS_CFG(80, 64, 1, 4, 2, 32, 4, 2); break;
+        case 4: XRS_CFG(32, 32, 2, 1, 1, 32, 2, 2); break;
         default:
             if constexpr (kTune) {
                 switch (cfg) {
-                    case 5: XRS_CFG(64, 64, 2, 2, 2, 64, 2); break;
-                    case 6: XRS_CFG(64, 64, 2, 2, 2, 32, 2); break;
-                    case 7: XRS_CFG(64, 80, 4, 1, 2, 32, 2); break;
-                    case 8: XRS_CFG(128, 128, 2, 4, 1, 32, 4); break;
-                    case 9: XRS_CFG(80, 64, 1, 4, 2, 32, 2); break;
-                    case 10: XRS_CFG(64, 64, 2, 2, 4, 64, 2); break;
-                    case 11: XRS_CFG(32, 80, 2, 1, 2, 32, 4); break;
-                    default: XRS_CFG(80, 32, 1, 2, 2, 32, 4); break;
+                    case 5: XRS_CFG(64, 64, 2, 2, 2, 64, 2, 2); break;
+                    case 6: XRS_CFG(64, 64, 2, 2, 2, 32, 2, 2); break;
+                    case 7: XRS_CFG(64, 80, 4, 1, 2, 32, 2, 2); break;
+                    case 8: XRS_CFG(128, 128, 2, 4, 1, 32, 4, 3); break;
+                    case 9: XRS_CFG(80, 64, 1, 4, 2, 32, 2, 2); break;
+                    case 10: XRS_CFG(64, 64, 2, 2, 2, 32, 4, 3); break;
+                    case 11: XRS_CFG(64, 80, 4, 1, 2, 32, 4, 3); break;
+                    default: XRS_CFG(80, 64, 1, 4, 2, 32, 4, 3); break;
                 }
             }
             break;
