@@ -284,6 +284,20 @@ int xrs_tt_shard(xrs_handle_t handle, size_t d, const size_t* n_global, int worl
 int xrs_tt_round_sharded(xrs_handle_t handle, size_t d, const size_t* n_local, size_t* r, double** cores,
                          const size_t* max_ranks, double eps, xrs_allreduce_fn allreduce, void* ctx, int* certified);
 
+/** Mode-sharded TT round for every input: the ranks' layout is given (world ranks, this one is
+ *  `rank`; every rank holds a contiguous block of each mode, blocks in rank order -- the layout of
+ *  xerus_amd.dist.mode_partition or any other), so besides the chain round and the certified truncation
+ *  (xrs_tt_round_sharded) it also runs the sharded general round (any spectrum and eps: shifted
+ *  CholeskyQR3 + Jacobi SVDs with device-side rank cuts, ttNetwork.cpp:644-665 semantics). Cores whose
+ *  unfolding spans the ranks' blocks -- tall right edges (r_k > n_k r_{k+1}, e.g. after x + y) and the
+ *  structural-excess QC steps at the left end -- are gathered by one all-reduce of a zero-padded core
+ *  (small: bounded by r^2) and factorised replicated. *path = XRS_ROUND_CHAIN / _TRUNCATE / _GENERAL on
+ *  success, 0 if every certificate failed (then the left-end QC steps may have been applied: the cores
+ *  represent the same tensor; gather and use xrs_tt_round). world * d <= 2048. */
+int xrs_tt_round_sharded_ex(xrs_handle_t handle, size_t d, const size_t* n_local, size_t* r, double** cores,
+                            const size_t* max_ranks, double eps, int world, int rank, xrs_allreduce_fn allreduce,
+                            void* ctx, int* path);
+
 /** <x,y> of two TTs mode-sharded identically (two-ended zipper: one all-reduce per step for both
  *  environments, ceil(d/2) in all for d >= 4; one per component below). */
 int xrs_tt_dot_sharded(xrs_handle_t handle, double* result, size_t d, const size_t* n_local, const size_t* rx,

@@ -1,0 +1,139 @@
+"""Sharded truncating rounds that used to gather onto one device: xrs_tt_round_sharded_ex over
+world 2 / 3 gloo ranks, all on the box's one GPU.
+
+  - (x + y).round(128) at the BASELINE configs[2] shape (order 10, n = 20, rank 128 each): the sum's left-end
+    structural excess (QC steps on the gathered core) and its tall right edge (gathered, replicated);
+  - a graded spectrum (raw cores, right rank index scaled by 0.8^j) round(64) and round(eps = 1e-8): the
+    sharded general round (shifted CholeskyQR3 + Jacobi SVDs, device-side rank cuts);
+  - a small x + y over 3 ranks with uneven mode blocks (n = 5: 2 / 2 / 1 slices).
+
+Reference: TTNetwork::round (ttNetwork.cpp:644-665), TTNetwork::operator+= (ttNetwork.cpp:797-847); the
+sharded form is new design. Bars: the round stays sharded (no gather); the oracle's ranks;
+truncation error within 1e-6 ||s|| of the oracle's, and the result within 1e-6 ||s|| of the oracle's
+result where the kept subspace is unique (the graded spectra); every rank holds the same result.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cases(ref):
+    """name -> (full cores, max ranks, eps); deterministic (the oracle's Rng)."""
+    out = {}
+    d, n, r = 10, 20, 128
+    ranks = bench.tt_ranks(d, n, r)[1:-1]
+    x = ref.TT.random_raw([n] * d, ranks, ref.Rng(21))
+    y = ref.TT.random_raw([n] * d, ranks, ref.Rng(22))
+    out["sum128"] = (ref.tt_add(x, y).cores, [128] * (d - 1), 8 * np.finfo(float).eps)
+    g = ref.TT.random_raw([n] * d, ranks, ref.Rng(23))
+    gc = [c.copy() for c in g.cores]
+    for k in range(d - 1):
+        gc[k] = gc[k] * (0.8 ** np.arange(gc[k].shape[2]))[None, None, :]
+    out["graded64"] = (gc, [64] * (d - 1), 8 * np.finfo(float).eps)
+    out["graded_eps"] = (gc, [2 ** 62] * (d - 1), 1e-8)
+    return out
+
+
+def _small_cases(ref):
+    d, n = 5, 5
+    ranks = bench.tt_ranks(d, n, 6)[1:-1]
+    x = ref.TT.random_raw([n] * d, ranks, ref.Rng(31))
+    y = ref.TT.random_raw([n] * d, ranks, ref.Rng(32))
+    return {"small_sum": (ref.tt_add(x, y).cores, [4] * (d - 1), 8 * np.finfo(float).eps)}
+
+
+def _worker(rank, world, port, which, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import xerus_ref as ref
+        from ttutil import tt_diff_norm
+        from xerus_amd import capi
+        from xerus_amd import dist as xd
+
+        torch.cuda.set_device(0)
+        h = capi.Handle(0)
+        comm = xd.TorchAllReduce()
+        cases = _cases(ref) if which == "big" else _small_cases(ref)
+        res = {}
+        for name, (cores, mr, eps) in cases.items():
+            st = xd.ShardedTT.from_full_cores(h, cores, world, rank)
+            path = st.round_sharded(mr, comm, eps)
+            full = st.gather_device(comm)
+            fc = full.cores()
+            rec = {"path": path, "ranks": list(full.r), "checksum": float(sum(np.abs(c).sum() for c in fc))}
+            if rank == 0:
+                e, nrm = tt_diff_norm(fc, cores)
+                rec["err"], rec["nrm"] = e, nrm
+                g = capi.TTDevice.from_cores(h, cores)
+                g.round(mr, eps)
+                rec["single_path"] = h.last_round_path()
+                rec["diff_single"] = tt_diff_norm(fc, g.cores())[0] / nrm
+                xo = ref.TT([c.copy() for c in cores])
+                xo.round(mr, eps)
+                rec["oracle_ranks"] = list(xo.ranks)
+                rec["oracle_err"] = tt_diff_norm(xo.cores, cores)[0]
+                rec["diff_oracle"] = tt_diff_norm(fc, xo.cores)[0] / nrm
+                g.free()
+            full.free()
+            st.local.free()
+            res[name] = rec
+        out[rank] = res
+        h.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, which):
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), which, out), nprocs=world, join=True)
+    return dict(out)
+
+
+def _check(out, world, unique):
+    r0 = out[0]
+    for name, rec in r0.items():
+        assert rec["path"] in ("chain", "truncate", "general"), (name, rec["path"])
+        for q in range(1, world):
+            assert out[q][name]["path"] == rec["path"]
+            assert out[q][name]["ranks"] == rec["ranks"]
+            assert out[q][name]["checksum"] == rec["checksum"]   # the same gathered result on every rank
+        assert rec["ranks"][1:-1] == rec["oracle_ranks"], (name, rec["ranks"], rec["oracle_ranks"])
+        nrm = rec["nrm"]
+        assert abs(rec["err"] - rec["oracle_err"]) <= 1e-6 * nrm, (name, rec["err"] / nrm, rec["oracle_err"] / nrm)
+        assert rec["diff_single"] <= 1e-8, (name, rec["diff_single"])
+        if name in unique:
+            assert rec["diff_oracle"] <= 1e-6, (name, rec["diff_oracle"])
+        print(f"{name} (world {world}): path {rec['path']}, ranks {rec['ranks'][1:-1]}, error {rec['err'] / nrm:.6e} "
+              f"(oracle {rec['oracle_err'] / nrm:.6e}), vs single GPU {rec['diff_single']:.2e}, "
+              f"vs oracle {rec['diff_oracle']:.2e}")
+
+
+def test_sharded_sum_and_graded_rounds_world2():
+    out = _run(2, "big")
+    _check(out, 2, unique=("graded64", "graded_eps"))
+    assert out[0]["graded64"]["path"] == "general"
+    assert out[0]["graded_eps"]["path"] == "general"
+
+
+def test_sharded_small_sum_world3_uneven():
+    out = _run(3, "small")
+    _check(out, 3, unique=())

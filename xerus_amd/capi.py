@@ -72,6 +72,8 @@ SIGNATURES = {
                                  C.POINTER(_SZ), C.POINTER(_DP)]),
     "xrs_tt_round_sharded": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
                                        C.c_double, _DP, _DP, C.POINTER(C.c_int)]),
+    "xrs_tt_round_sharded_ex": (C.c_int, [_DP, _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP), C.POINTER(_SZ),
+                                          C.c_double, C.c_int, C.c_int, _DP, _DP, C.POINTER(C.c_int)]),
     "xrs_tt_dot_sharded": (C.c_int, [_DP, C.POINTER(C.c_double), _SZ, C.POINTER(_SZ), C.POINTER(_SZ), C.POINTER(_DP),
                                      C.POINTER(_SZ), C.POINTER(_DP), _DP, _DP]),
     "xrs_tt_last_round_path": (C.c_int, [_DP]),

@@ -1273,8 +1273,36 @@ int xrs_tt_round_sharded(xrs_handle_t h, size_t d, const size_t* n_local, size_t
         t.shard_mode = true;
         t.ar = allreduce;   // null: one rank
         t.ar_ctx = ctx;
-        // no cut possible: the chain round; ranks to cut: the certified truncation (wide edges only)
+        // no cut possible: the chain round; ranks to cut: the certified truncation (the ranks' order is not
+        // known here: tall right edges and left structural excess report uncertified; see xrs_tt_round_sharded_ex)
         *certified = (round_chain(t, max_ranks, eps) || round_truncate(t, max_ranks, eps)) ? 1 : 0;
+    });
+}
+
+int xrs_tt_round_sharded_ex(xrs_handle_t h, size_t d, const size_t* n_local, size_t* r, double** cores,
+                            const size_t* max_ranks, double eps, int world, int rank, xrs_allreduce_fn allreduce,
+                            void* ctx, int* path) {
+    return guarded([&] {
+        XRS_REQUIRE(h && path, "null argument");
+        XRS_REQUIRE(d >= 2 && n_local && r && cores && max_ranks, "null TT description");
+        XRS_REQUIRE(r[0] == 1 && r[d] == 1, "boundary ranks must be 1");
+        XRS_REQUIRE(world >= 1 && rank >= 0 && rank < world, "world / rank out of range");
+        XRS_REQUIRE(size_t(world) * d <= 2048, "world * d above 2048");
+        XRS_REQUIRE(eps < 1.0 && eps >= 0.0, "_eps must be smaller than one.");
+        for (size_t k = 0; k + 1 < d; ++k)
+            XRS_REQUIRE(max_ranks[k] > 0, "Trying to round a TTTensor to rank 0 is not possible.");
+        TT t{h, d, n_local, r, cores};
+        t.shard_mode = true;
+        t.ar = allreduce;   // null: one rank
+        t.ar_ctx = ctx;
+        t.world = world;
+        t.rank = rank;
+        static const bool no_general = std::getenv("XRS_NO_GENERAL_ROUND") != nullptr;
+        *path = 0;
+        if (round_chain(t, max_ranks, eps)) *path = XRS_ROUND_CHAIN;
+        else if (round_truncate(t, max_ranks, eps)) *path = XRS_ROUND_TRUNCATE;
+        else if (!no_general && round_general(t, max_ranks, eps)) *path = XRS_ROUND_GENERAL;
+        if (*path) h->last_round_path = *path;
     });
 }
 

@@ -36,6 +36,11 @@ struct TT {
     bool shard_mode = false;
     xrs_allreduce_fn ar = nullptr;
     void* ar_ctx = nullptr;
+    // the ranks' layout (xrs_tt_round_sharded_ex): world > 0 when known; each rank holds a contiguous block
+    // of every mode, blocks in rank order. Unknown (0): cores whose unfolding spans the ranks' blocks
+    // (tall right edges, structural-excess QC steps) cannot be gathered and the round reports uncertified
+    int world = 0;
+    int rank = 0;
     bool sharded() const { return shard_mode; }
     void reduce(double* buf, size_t count) const {
         if (!ar) return;
@@ -45,6 +50,18 @@ struct TT {
         XRS_REQUIRE(rc == 0, "all-reduce callback failed");
     }
 };
+
+// Mode layout of a sharded TT (tt_trunc.hip): global mode sizes ng, this rank's first slice off per mode;
+// known = false when the ranks' order is unknown (world 0) -- then off is meaningless.
+struct ShardLayout {
+    std::vector<size_t> ng, off;
+    bool known = true;
+};
+ShardLayout shard_layout(TT& t);
+void gather_core(TT& t, const double* local, size_t a, size_t nl, size_t ng, size_t b, size_t off, double* full);
+void slice_core(TT& t, const double* full, size_t a, size_t ng, size_t b, size_t off, size_t nl, double* local);
+void transfer_right_sharded(TT& t, size_t k, const ShardLayout& lay);
+void remove_left_excess(TT& t, const ShardLayout& lay);
 
 // reduce_to_maximal_ranks (ttNetwork.cpp:370-402) of the internal ranks; true if any rank exceeds it
 std::vector<size_t> maximal_ranks(const TT& t);

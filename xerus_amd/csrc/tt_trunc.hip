@@ -232,6 +232,92 @@ void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<
 
 }  // namespace
 
+// Global mode sizes and this rank's first slice per mode (sharded: one all-reduce of a world x d table
+// with this rank's slice counts in its row, one host synchronisation; world unknown: the sums only).
+ShardLayout shard_layout(TT& t) {
+    const size_t d = t.d;
+    ShardLayout lay;
+    lay.ng.assign(t.n, t.n + d);
+    lay.off.assign(d, 0);
+    lay.known = !t.sharded();
+    if (!t.sharded()) return lay;
+    xrs_handle_t h = t.h;
+    const size_t w = t.world > 0 ? size_t(t.world) : 1, me = t.world > 0 ? size_t(t.rank) : 0;
+    XRS_REQUIRE(w * d <= 2048 && me < w, "shard_layout: world / rank out of range");
+    double* hn = static_cast<double*>(h->host_scratch) + 3400;   // (pinned scratch: doubles 3400 .. 5448)
+    for (size_t i = 0; i < w * d; ++i) hn[i] = 0.0;
+    for (size_t k = 0; k < d; ++k) hn[me * d + k] = double(t.n[k]);
+    DevBuf tab(h, w * d * 8);
+    XRS_HIP(hipMemcpyAsync(tab.d(), hn, w * d * 8, hipMemcpyHostToDevice, h->stream));
+    t.reduce(tab.d(), w * d);
+    XRS_HIP(hipMemcpyAsync(hn, tab.d(), w * d * 8, hipMemcpyDeviceToHost, h->stream));
+    host_wait(h);
+    for (size_t k = 0; k < d; ++k) {
+        size_t s = 0, o = 0;
+        for (size_t q = 0; q < w; ++q) {
+            const size_t c = size_t(hn[q * d + k] + 0.5);
+            s += c;
+            if (q < me) o += c;
+        }
+        lay.ng[k] = s;
+        lay.off[k] = o;
+    }
+    lay.known = t.world > 0;
+    return lay;
+}
+
+// Full core (a, ng, b) on every rank from this rank's slices (a, nl, b) at mode offset `off`: zeros
+// elsewhere, completed by one all-reduce (each entry has exactly one non-zero contribution: exact).
+void gather_core(TT& t, const double* local, size_t a, size_t nl, size_t ng, size_t b, size_t off, double* full) {
+    xrs_handle_t h = t.h;
+    XRS_HIP(hipMemsetAsync(full, 0, a * ng * b * 8, h->stream));
+    if (nl && a && b)
+        XRS_HIP(hipMemcpy2DAsync(full + off * b, ng * b * 8, local, nl * b * 8, nl * b * 8, a, hipMemcpyDeviceToDevice, h->stream));
+    t.reduce(full, a * ng * b);
+}
+
+// This rank's slices (a, nl, b) of a full core (a, ng, b).
+void slice_core(TT& t, const double* full, size_t a, size_t ng, size_t b, size_t off, size_t nl, double* local) {
+    if (!(nl && a && b)) return;
+    XRS_HIP(hipMemcpy2DAsync(local, nl * b * 8, full + off * b, ng * b * 8, nl * b * 8, a, hipMemcpyDeviceToDevice, t.h->stream));
+}
+
+// transfer_right (QC of core k, R into core k + 1) of a sharded TT: the left unfolding's rows are the
+// ranks' mode blocks, so core k is gathered (small: a structural excess r_{k+1} > r_k n_k bounds it by
+// r_{k+1}^2), factorised identically on every rank (deterministic kernels, same rank decision) and sliced.
+void transfer_right_sharded(TT& t, size_t k, const ShardLayout& lay) {
+    XRS_REQUIRE(lay.known, "transfer_right_sharded: rank layout unknown");
+    const size_t a = t.r[k], nl = t.n[k], ng = lay.ng[k], b = t.r[k + 1];
+    const size_t m = a * ng, kmax = std::min(m, b);
+    double* full = t.alloc(m * b);
+    gather_core(t, t.core[k], a, nl, ng, b, lay.off[k], full);
+    double* Q = t.alloc(m * kmax);
+    double* C = t.alloc(kmax * b);
+    const size_t rank = qc(t.h, full, m, b, Q, C);
+    t.release(full);
+    double* Ql = t.alloc(a * nl * rank);
+    slice_core(t, Q, a, ng, rank, lay.off[k], nl, Ql);
+    const size_t ncols = t.cols_right(k + 1);
+    double* nxt = t.alloc(rank * ncols);
+    gemm(t.h, nxt, rank, ncols, 1.0, C, b, false, b, t.core[k + 1], ncols, false);
+    t.release(C);
+    t.release(Q);
+    t.replace(k, Ql);
+    t.replace(k + 1, nxt);
+    t.r[k + 1] = rank;
+}
+
+// 1a of both rounds: structural excess (a wide left unfolding, r_{k+1} > r_k n_k, e.g. the boundary edges
+// of x + y) removed by the reference's own QC steps (exact rank rule, host syncs). Sharded with an unknown
+// layout: left in place (the left Gram is then singular, the certificate fails, the caller gathers).
+void remove_left_excess(TT& t, const ShardLayout& lay) {
+    for (size_t k = 0; k + 1 < t.d; ++k) {
+        if (!(t.r[k + 1] > t.r[k] * lay.ng[k])) continue;
+        if (!t.sharded()) transfer_right(t, k, true);
+        else if (lay.known) transfer_right_sharded(t, k, lay);
+    }
+}
+
 bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
@@ -242,13 +328,12 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     for (size_t k = 1; k < d; ++k)
         if (t.r[k] > kHugeMax) return false;
 
+    // global mode sizes and this rank's slice offsets (sharded: one all-reduce + host sync)
+    const ShardLayout lay = shard_layout(t);
+    const std::vector<size_t>& ng = lay.ng;
     // 1a. structural excess (a wide left unfolding, r_{k+1} > r_k n_k, e.g. the boundary edges of x + y):
-    //     the reference's own QC steps there (exact rank rule, host syncs)
-    //     (sharded: not available -- an excess makes the left Gram singular, the certificate fails and the
-    //     caller rounds the gathered TT instead)
-    if (!t.sharded())
-        for (size_t k = 0; k + 1 < d; ++k)
-            if (t.r[k + 1] > t.r[k] * t.n[k]) transfer_right(t, k, true);
+    //     the reference's own QC steps there (exact rank rule, host syncs; sharded: on the gathered core)
+    remove_left_excess(t, lay);
 
     Sweep sw(t);
     // statuses: factorisations from 0 up, Jacobi convergence at kJacobiSlot + edge
@@ -257,16 +342,6 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
     int* status = st.as<int>();
     int nst = 0;
     XRS_HIP(hipMemsetAsync(status, 0, kStatusWords * 4, h->stream));
-    // global mode sizes (sharded: the sum of every rank's slice counts, read at the first check point)
-    std::vector<size_t> ng(t.n, t.n + d);
-    double* nsum = nullptr;
-    if (t.sharded()) {
-        double* hn = static_cast<double*>(h->host_scratch) + 3400;
-        for (size_t k = 0; k < d; ++k) hn[k] = double(t.n[k]);
-        nsum = sw.buf(d);
-        XRS_HIP(hipMemcpyAsync(nsum, hn, d * 8, hipMemcpyHostToDevice, h->stream));
-        t.reduce(nsum, d);
-    }
 
     // 1b. left chain pass (certified), and a second one on its output when a single CholeskyQR pass over
     //     the train left the cores short of orthonormal (kappa^2 u > tol: CholeskyQR2 on the whole train)
@@ -290,10 +365,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         const int nchk = int(d - 1) * 16;
         XRS_HIP(hipMemcpyAsync(hs, status, size_t(nst) * 4, hipMemcpyDeviceToHost, h->stream));
         XRS_HIP(hipMemcpyAsync(hd, devb.d(), size_t(nchk) * 8, hipMemcpyDeviceToHost, h->stream));
-        if (nsum) XRS_HIP(hipMemcpyAsync(hd + 1024, nsum, d * 8, hipMemcpyDeviceToHost, h->stream));
         host_wait(h);
-        if (nsum)
-            for (size_t k = 0; k < d; ++k) ng[k] = size_t(hd[1024 + k] + 0.5);
         bool ok = true;
         for (int i = 0; i < nst; ++i) ok = ok && hs[i] == 0;
         worst = 0.0;
@@ -341,8 +413,11 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
         const size_t r = rr[k], N = t.n[k] * rr[k + 1], Ng = ng[k] * rr[k + 1];   // local / global columns
         const size_t kk = std::min({r, Ng, max_ranks[k - 1]});
         const bool wide = r <= Ng;
-        if (!wide && t.sharded()) {   // the N x N Gram of a tall edge spans the ranks' column blocks
-            if (dbg) std::fprintf(stderr, "round_truncate: sharded tall edge %zu -> not certified\n", k);
+        // sharded tall edge: the N x N Gram spans the ranks' column blocks -- the core (r x Ng, small: Ng < r)
+        // is gathered and the edge runs replicated on every rank (deterministic kernels: identical results)
+        const bool tall_gather = !wide && t.sharded();
+        if (tall_gather && !lay.known) {
+            if (dbg) std::fprintf(stderr, "round_truncate: sharded tall edge %zu, rank layout unknown -> not certified\n", k);
             if (side_used) {   // the side stream may still read this sweep's buffers
                 XRS_HIP(hipEventRecord(h->ev_join[0], h->side_stream[0]));
                 XRS_HIP(hipStreamWaitEvent(h->stream, h->ev_join[0], 0));
@@ -350,11 +425,16 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
             sw.discard();
             return false;
         }
-        const size_t g = wide ? r : N;
+        const size_t Nw = tall_gather ? Ng : N;   // columns of the edge matrix as factorised here
+        const size_t g = wide ? r : Nw;
         double* B = A[k];
+        if (tall_gather) {
+            B = sw.buf(r * Nw);
+            gather_core(t, A[k], r, t.n[k], ng[k], rr[k + 1], lay.off[k], B);
+        }
         double* P = sw.buf(g * g);
         if (wide) gemm_sym(h, P, g, 1.0, B, N, false, N, B, N, true);
-        else gemm_sym(h, P, g, 1.0, B, N, true, r, B, N, false);
+        else gemm_sym(h, P, g, 1.0, B, Nw, true, r, B, Nw, false);
         if (wide) t.reduce(P, g * g);   // sharded: sum over the mode slices
         // the kept subspace: P's kk dominant eigenvectors. The certificate chol(P - tau tr(P) I) bounds
         // kappa(P) <= 4 / tau, so P's eigenvectors are accurate to u kappa-free relative gaps and no eps cut
@@ -386,7 +466,7 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
             nst += chol_status_count(cj);
         }
         double* S = sw.buf(g);
-        double* Vt = wide ? sw.buf(g * g) : sw.core(g * g);
+        double* Vt = (wide || tall_gather) ? sw.buf(g * g) : sw.core(g * g);
         int* js = status + kJacobiSlot + int(jst.size());
         if (use_eig) sym_eig_top(h, P, int(g), int(g), int(kk), S, nullptr, Vt, int(g), js);   // (S <- lambda)
         else jacobi_vt(h, L, int(g), true, int(g), int(g), S, Vt, int(g), js);
@@ -401,13 +481,18 @@ bool round_truncate(TT& t, const size_t* max_ranks, double eps) {
             newk = sw.core(kk * N);
             gemm(h, newk, kk, N, 1.0, M, r, false, r, B, N, false);               // S^{-1} U^T B = Vt_B[:kk]
         } else {      // Vt holds the right singular vectors of L^T = those of B (B = Q L^T)
-            newk = Vt;                                                            // first kk rows
-            gemm(h, Tk, r, kk, 1.0, B, N, false, N, Vt, N, true);                 // U S = B Vt_kk^T
+            if (tall_gather) {   // this rank's columns (mode slices) of the first kk rows
+                newk = sw.core(kk * N);
+                slice_core(t, Vt, kk, ng[k], rr[k + 1], lay.off[k], t.n[k], newk);
+            } else {
+                newk = Vt;                                                        // first kk rows
+            }
+            gemm(h, Tk, r, kk, 1.0, B, Nw, false, Nw, Vt, Nw, true);              // U S = B Vt_kk^T
         }
         const size_t prow = t.rows_left(k - 1);   // = rr[k-1] * n[k-1] (left ranks unchanged so far)
         double* prevk = sw.core(prow * kk);
         gemm(h, prevk, prow, kk, 1.0, A[k - 1], r, false, r, Tk, kk, false);
-        sw.drop(B);
+        sw.drop(A[k]);
         sw.drop(A[k - 1]);
         A[k] = newk;
         A[k - 1] = prevk;
@@ -579,9 +664,10 @@ unsigned grid_for(size_t elems) { return unsigned(std::min<size_t>(std::max<size
 // m <= n) = L Q (RL = L, lower, m x m). st[0..3) potrf statuses; trG[0] = ||A||_F^2; with Rinv, the
 // explicit inverse of the triangular factor (tall: R^{-1} transposed, i.e. L3^{-1} L2^{-1} L1^{-1} --
 // same Frobenius norm). N = min(m, n) <= 512. pad_kk (tall only): the columns p with p % pad_b >= *pad_kk are
-// known to be zero (k_pad_diag).
+// known to be zero (k_pad_diag). reduce (sharded): the Grams are sums over the ranks' blocks of the long
+// dimension, all-reduced; Mg = its global length (the shift must be the same on every rank).
 void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q, double* RL, int* st, double* trG, double* Rinv,
-           const int* pad_kk = nullptr, int pad_b = 1) {
+           const int* pad_kk = nullptr, int pad_b = 1, bool reduce = false, size_t Mg = 0) {
     xrs_handle_t h = sw.t.h;
     const size_t N = wide ? m : n, M = wide ? n : m;
     const int Ni = int(N);
@@ -591,12 +677,13 @@ void scqr3(Sweep& sw, const double* A, size_t m, size_t n, bool wide, double* Q,
     double* X1 = sw.buf(m * n);
     double* X2 = sw.buf(m * n);
     double* info = sw.buf(4);
-    const double s_rel = 11.0 * (double(M) * N + double(N) * (N + 1)) * kUnit;
+    const double s_rel = 11.0 * (double(Mg ? Mg : M) * N + double(N) * (N + 1)) * kUnit;
     const double* cur = A;
     double* outs[3] = {X1, X2, Q};
     for (int p = 0; p < 3; ++p) {
         if (wide) gemm_sym(h, L[p], N, 1.0, cur, n, false, M, cur, n, true);   // X X^T
         else gemm_sym(h, L[p], N, 1.0, cur, n, true, M, cur, n, false);        // X^T X
+        if (reduce) sw.t.reduce(L[p], N * N);
         if (pad_kk && !wide) {
             hipLaunchKernelGGL(k_pad_diag, dim3(1), dim3(256), 0, h->stream, L[p], Ni, pad_b, pad_kk, true);
             check_launch("k_pad_diag");
@@ -639,13 +726,16 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
     static const bool dbg = std::getenv("XRS_DEBUG_ROUND") != nullptr;
-    if (d < 2 || d > 64 || t.sharded()) return false;
+    if (d < 2 || d > 64) return false;
     for (size_t k = 1; k < d; ++k)
         if (t.r[k] > size_t(kSmallMax)) return false;
 
-    // structural excess at the left end (r_{k+1} > r_k n_k): the reference's own QC steps (as round_truncate)
-    for (size_t k = 0; k + 1 < d; ++k)
-        if (t.r[k + 1] > t.r[k] * t.n[k]) transfer_right(t, k, true);
+    // global mode sizes / this rank's slice offsets (sharded: one all-reduce + host sync); structural excess
+    // at the left end (r_{k+1} > r_k n_k): the reference's own QC steps (as round_truncate)
+    const ShardLayout lay = shard_layout(t);
+    const std::vector<size_t>& ng = lay.ng;
+    const bool sharded = t.sharded();
+    remove_left_excess(t, lay);
 
     Sweep sw(t);
     constexpr int kSlots = 2048;
@@ -668,7 +758,7 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
     {
         size_t mmax = 1, rmax = 1;
         for (size_t k = 0; k < d; ++k) {
-            mmax = std::max(mmax, rr[k] * t.n[k]);
+            mmax = std::max(mmax, rr[k] * ng[k]);
             rmax = std::max(rmax, rr[k + 1]);
         }
         const double s_rel = 11.0 * kUnit * (double(mmax) * double(d) + double(rmax) * double(rmax + 1));
@@ -737,12 +827,15 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
     // 1b. otherwise core by core: A_k = Q_k, next = R_k core_{k+1}, each by shifted CholeskyQR3
     for (size_t k = 0; !chain_ok && k + 1 < d; ++k) {
         const size_t m = rr[k] * t.n[k], b = rr[k + 1];
-        XRS_REQUIRE(m >= b, "round_general: structural excess left after the QC steps");
+        if (rr[k] * ng[k] < b) {   // (sharded with an unknown layout: the excess could not be removed)
+            sw.discard();
+            return false;
+        }
         double* Q = sw.core(m * b);
         double* R = sw.buf(b * b);
         double* Rinv = sw.buf(b * b);
         double* trG = sw.buf(1);
-        scqr3(sw, A[k], m, b, false, Q, R, st + nst, trG, Rinv);
+        scqr3(sw, A[k], m, b, false, Q, R, st + nst, trG, Rinv, nullptr, 1, sharded, rr[k] * ng[k]);
         nst += 3;
         hipLaunchKernelGGL(k_rank_cert, dim3(1), dim3(256), 0, h->stream, Rinv, int(b), trG, 32.0 * kUnit, st + nst);
         check_launch("k_rank_cert");
@@ -766,13 +859,13 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         // are masked, k_pad_diag). When the cut can go that deep (an eps cut, or maxRank n_k < r_k), read kk
         // (one synchronisation) and compact core_k to its kk right columns; core_{k+1}'s first kk rows
         // already hold the kept rows.
-        if (k + 1 < d && g[k] > t.n[k] && (eps > kDefaultEps || max_ranks[k] * t.n[k] < g[k])) {
+        if (k + 1 < d && g[k] > ng[k] && (eps > kDefaultEps || max_ranks[k] * ng[k] < g[k])) {
             int* kh = hs + kSlots - 1;
             XRS_HIP(hipMemcpyAsync(kh, st + kRank + int(k + 1), 4, hipMemcpyDeviceToHost, h->stream));
             host_wait(h);
             ++nsync;
             const size_t v = size_t(*kh);
-            if (*kh >= 1 && v < g[k + 1] && v * t.n[k] < g[k]) {
+            if (*kh >= 1 && v < g[k + 1] && v * ng[k] < g[k]) {
                 const size_t rows = g[k] * t.n[k], gb = g[k + 1];
                 double* Cc = sw.core(rows * v);
                 XRS_HIP(hipMemcpy2DAsync(Cc, v * 8, A[k], gb * 8, v * 8, rows, hipMemcpyDeviceToDevice, h->stream));
@@ -781,15 +874,27 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
                 g[k + 1] = v;
             }
         }
-        const size_t r = g[k], N = t.n[k] * g[k + 1];
-        const bool wide = r <= N;
-        const size_t gg = wide ? r : N;
+        const size_t r = g[k], N = t.n[k] * g[k + 1], Ng = ng[k] * g[k + 1];   // local / global columns
+        const bool wide = r <= Ng;
+        // sharded tall edge: gathered (r x Ng, Ng < r) and factorised replicated (as round_truncate)
+        const bool tall_gather = !wide && sharded;
+        if (tall_gather && !lay.known) {
+            if (dbg) std::fprintf(stderr, "round_general: sharded tall edge %zu, rank layout unknown -> not certified\n", k);
+            sw.discard();
+            return false;
+        }
+        const size_t Nw = tall_gather ? Ng : N;
+        const size_t gg = wide ? r : Nw;
         double* B = A[k];
-        double* Qf = sw.buf(r * N);
+        if (tall_gather) {
+            B = sw.buf(r * Nw);
+            gather_core(t, A[k], r, t.n[k], ng[k], g[k + 1], lay.off[k], B);
+        }
+        double* Qf = sw.buf(r * Nw);
         double* F = sw.buf(gg * gg);
         // (tall edge after a cut of edge k + 1: its padded zero columns, k_pad_diag)
         const int* pad = (!wide && k + 1 < d) ? st + kRank + int(k + 1) : nullptr;
-        scqr3(sw, B, r, N, wide, Qf, F, st + nst, nullptr, nullptr, pad, int(g[k + 1]));
+        scqr3(sw, B, r, Nw, wide, Qf, F, st + nst, nullptr, nullptr, pad, int(g[k + 1]), wide && sharded, Ng);
         nst += 3;
         double* S = sw.buf(gg);
         double* V = sw.buf(gg * gg);
@@ -811,11 +916,12 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
             gemm(h, newk, gg, N, 1.0, V, gg, false, gg, Qf, N, false);
             gemm(h, T, r, gg, 1.0, F, gg, false, gg, V, gg, true);
         } else {      // B = Q R, R = U S V^T: core_k <- V_kk^T, core_{k-1} <- core_{k-1} (B V_kk)
-            XRS_HIP(hipMemcpyAsync(newk, V, gg * N * 8, hipMemcpyDeviceToDevice, h->stream));
-            gemm(h, T, r, gg, 1.0, B, N, false, N, V, N, true);
+            if (tall_gather) slice_core(t, V, gg, ng[k], g[k + 1], lay.off[k], t.n[k], newk);   // this rank's columns
+            else XRS_HIP(hipMemcpyAsync(newk, V, gg * N * 8, hipMemcpyDeviceToDevice, h->stream));
+            gemm(h, T, r, gg, 1.0, B, Nw, false, Nw, V, Nw, true);
         }
         gemm(h, prevk, prow, gg, 1.0, A[k - 1], r, false, r, T, gg, false);
-        sw.drop(B);
+        sw.drop(A[k]);
         sw.drop(A[k - 1]);
         A[k] = newk;
         A[k - 1] = prevk;

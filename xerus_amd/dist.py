@@ -208,6 +208,26 @@ class ShardedTT:
             t.canonicalized, t.core_position = True, 0
         return bool(cert.value)
 
+    def round_sharded(self, max_ranks, comm, eps: float = 8 * np.finfo(float).eps) -> str:
+        """Sharded round for any spectrum (xrs_tt_round_sharded_ex: chain, certified truncation or the general
+        round, all on the slices; tall right edges and left-end QC steps on cores gathered by one all-reduce).
+        Returns "chain" / "truncate" / "general", or "" if every certificate failed (same tensor, left-end QC
+        steps possibly applied -- gather and round on one device then)."""
+        t = self.local
+        d = t.order
+        if isinstance(max_ranks, (int, np.integer)):
+            max_ranks = [int(max_ranks)] * (d - 1)
+        n, r, cores = t._arrays()
+        mr = capi._arr(list(max_ranks) + [1])
+        path = C.c_int(0)
+        st = self.handle.lib.xrs_tt_round_sharded_ex(self.handle.h, d, n, r, cores, mr, eps, self.world, self.rank,
+                                                     comm.c_fn, comm.ctx, C.byref(path))
+        t._writeback(r, cores)
+        capi._check("xrs_tt_round_sharded_ex", st)
+        if path.value:
+            t.canonicalized, t.core_position = True, 0
+        return {1: "chain", 2: "truncate", 4: "general"}.get(path.value, "")
+
     def dot(self, other: "ShardedTT", comm) -> float:
         x, y = self.local, other.local
         if self.dims != other.dims or x.dims != y.dims:
@@ -235,10 +255,11 @@ class ShardedTT:
         return capi.TTDevice(self.handle, self.dims, t.r, [p or 0 for p in out[:]], t.canonicalized, t.core_position)
 
     def round_any(self, max_ranks, comm, eps: float = 8 * np.finfo(float).eps) -> str:
-        """The round for every input: the certified sharded round ("sharded"), else the TT is gathered on the
+        """The round for every input: the sharded round ("sharded": chain, certified truncation or general
+        round, ShardedTT.round_sharded), else the TT is gathered on the
         device of every rank, rounded there by the single-GPU round (identical inputs and deterministic
         kernels: identical results on every rank) and re-sharded locally ("gathered")."""
-        if self.round(max_ranks, comm, eps):
+        if self.round_sharded(max_ranks, comm, eps):
             return "sharded"
         full = self.gather_device(comm)
         full.round(max_ranks, eps)
