@@ -60,7 +60,7 @@ void jacobi_svd_rows(xrs_handle_t h, const double* W, int p, int q, double* U, d
 // cycles per cross-round phase (dot, rotation, update, barrier) and its rotation count -- status_dev
 // must then hold 9 ints. Enqueued only.
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
-               int* status_dev, int max_sweeps = 40, int kernel = 0, bool stamps = false);
+               int* status_dev, int max_sweeps = 40, int kernel = 0, bool stamps = false, bool early = false);
 bool jacobi_vt_fits_lds(int p, int q);
 // Full SVD of the rows of W (p x q, p <= q, 32 ceil(q/32) + p <= 1024) by the block Jacobi kernel with
 // the rotations accumulated (svd.hip): W = U diag(S) Vt, U p x p orthogonal (row stride ldu), S
@@ -76,11 +76,13 @@ void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double
 void sym_tridiag(xrs_handle_t h, const double* A, int lda, int n, double* d, double* e);
 bool jacobi_usv_fits(int p, int q);
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
-                int* status_dev, int max_sweeps = 40);
+                int* status_dev, int max_sweeps = 40, bool early = false);
 // Right singular vectors (rows of Vt, g x g) and S of a triangular g x g factor F: lower (L of B = L Q) by
 // accumulated rotations on the rows of F^T, upper (R of B = Q R) on the rows of F. Enqueued only.
+// early: the block kernel's early stop (svd.hip kEarlyCos2: no confirming sweep after one whose rotations
+// were all below |cos| 1e-7) -- the truncation sweeps (tt_trunc.hip round_general)
 void jacobi_right_vectors(xrs_handle_t h, const double* F, int g, bool lower, double* S, double* Vt, int* status_dev,
-                          int max_sweeps = 40);
+                          int max_sweeps = 40, bool early = false);
 
 // Reads a Jacobi status word (synchronises) and returns it. -2 (a grid-barrier poll of the block kernel timed
 // out) means the outputs are invalid, not a convergence failure: rerun(kernel) recomputes them (kernel 1 = one

@@ -99,6 +99,14 @@ __device__ __forceinline__ void rotation(double a, double b, double c, double& s
     rotation(a, b, c, s, tau, tn);
 }
 
+// Early stop of the block kernel (flags & 2, the truncation sweeps): a sweep whose rotations all had
+// |cos| = |w_i . w_j| / (||w_i|| ||w_j||) <= 1e-7 ends the iteration. Cyclic Jacobi converges quadratically,
+// so the sweep that would follow rotates by ~1e-14 / (relative gap) at most: it only confirms convergence
+// (measured on the graded cfg3 edges: the 5th sweep's largest |cos| was 2e-10 .. 2e-8, the 6th rotated
+// nothing). The rows stay exactly a product of rotations (orthonormal V); the singular values move by
+// O(cos^2) relatively.
+constexpr double kEarlyCos2 = 1e-14;
+
 // rows padded with zeros to E * G (no bounds checks: the padding stays zero under rotations)
 template <int G, int E>
 __device__ __forceinline__ void load_row_full(double (&x)[E], const double* __restrict__ w, int l) {
@@ -117,7 +125,7 @@ __device__ __forceinline__ void store_row_full(const double (&x)[E], double* __r
 // The register core: the lane's E elements of each row (zero beyond q, which rotations keep zero)
 // (the inner products run over the first ew elements: the rest may carry accumulated rotations)
 template <int G, int E>
-__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E) {
+__device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], double tol2, int ew = E, bool* big = nullptr) {
     double a = 0.0, b = 0.0, c = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -131,6 +139,7 @@ __device__ __forceinline__ bool rotate_regs(double (&x)[E], double (&y)[E], doub
     b = gsum<G>(b);
     c = gsum<G>(c);
     if (!(c * c > tol2 * a * b)) return false;
+    if (big && c * c > kEarlyCos2 * a * b) *big = true;
     double s, tau;
     rotation(a, b, c, s, tau);
 #pragma unroll
@@ -307,7 +316,7 @@ __global__ void __launch_bounds__(SVG_THREADS) k_jacobi_vt_global(double* __rest
 // barrier that the polling wave joins -- no release/acquire fences (no L2 write-back or L1 invalidate
 // per round). The poll is bounded (status -2 instead of a hang if a workgroup were never scheduled).
 constexpr int SVB_G = 16, SVB_LDS = 16384, SVB_QMAX = 512;
-constexpr int SVB_SYNC_WORDS = 64;   // [0] barrier counter, [1 + sweep] rotated flags
+constexpr int SVB_SYNC_WORDS = 128;  // [0] barrier counter, [1 + sweep] rotated flags, [64 + sweep] |cos| > 1e-7 flags
 typedef int svb_v4i __attribute__((ext_vector_type(4)));
 constexpr int kBufCfg = 0x00020000;  // raw buffer descriptor word 3 (32-bit data format)
 constexpr int kSc1 = 16;             // cache policy: sc1 (write-through stores, L1-bypassing loads)
@@ -370,13 +379,13 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                                                                  double* __restrict__ S, double* __restrict__ Vt, int ldvt,
                                                                  double* __restrict__ U, int ldu, int* __restrict__ status, int flags) {
     constexpr int NT = BR * G, R2 = 2 * BR;
-    const bool stamps = (flags & 1) != 0;
+    const bool stamps = (flags & 1) != 0, early = (flags & 2) != 0;
     // diagnostics (stamps != 0, XRS_SVD_TIMING): cycles of thread 0 per cross-round phase -- dot + sum,
     // rotation parameters, update + store, barrier wait -- and the rotation count, into status[4..8]
     unsigned long long st_ph[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
     static_assert((BR & (BR - 1)) == 0 && BR >= 4, "BR: a power of two");
     __shared__ __attribute__((aligned(16))) double Ws[SVB_LDS];
-    __shared__ int rotated, err;
+    __shared__ int rotated, err, bigrot;
     __shared__ double bn[BR];   // squared norms of the bottom rows during the cross rounds
     __shared__ int part[NT / 64 > 0 ? NT / 64 : 1];
     const int tid = threadIdx.x, g = tid / G, l = tid % G;
@@ -414,8 +423,12 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
     int sweep = 0;
     bool converged = false;
     while (sweep < max_sweeps && !converged) {
-        if (tid == 0) rotated = 0;
+        if (tid == 0) {
+            rotated = 0;
+            bigrot = 0;
+        }
         __syncthreads();
+        bool big = false;   // (this thread's group rotated by |cos| > 1e-7 in this sweep)
         for (int t = 0; t < nb - 1; ++t) {
             if (t == 0) {
                 // first outer round of the sweep: the pairs inside each block (circle method over BR
@@ -427,7 +440,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                     double x[E], y[E];
                     load_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                     load_row_full<G, E>(y, Ws + (base + j) * ldw, l);
-                    if (rotate_regs<G, E>(x, y, tol2, ew)) {
+                    if (rotate_regs<G, E>(x, y, tol2, ew, &big)) {
                         store_row_full<G, E>(x, Ws + (base + i) * ldw, l);
                         store_row_full<G, E>(y, Ws + (base + j) * ldw, l);
                         if (l == 0) rotated = 1;
@@ -467,6 +480,7 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
                         if (e < ew) c4[e & 3] = fma(x[e], y[e], c4[e & 3]);
                     const double c = gsum<G>((c4[0] + c4[1]) + (c4[2] + c4[3]));
                     const bool do_rot = c * c > tol2 * a * b;
+                    big = big || (do_rot && c * c > kEarlyCos2 * a * b);
                     unsigned long long c1 = 0ull, c2 = 0ull;
                     if (stamps) {
                         c1 = __builtin_amdgcn_s_memtime() + (do_rot ? 0ull : 0ull);
@@ -523,8 +537,14 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
             const long long t0 = wall_clock64();
             if (top != 0) block_out<NT>(Ws, rs, top * bunits * 16, bunits, tid);
             block_out<NT>(Wb, rs, bot * bunits * 16, bunits, tid);
+            if (t == nb - 2 && early) {
+                if (big && l == 0) bigrot = 1;
+                __syncthreads();
+            }
             if (t == nb - 2 && tid == 0 && rotated)
                 __hip_atomic_fetch_or(&sync[1 + sweep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t == nb - 2 && tid == 0 && early && bigrot)
+                __hip_atomic_fetch_or(&sync[64 + sweep], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const long long t1 = wall_clock64();
             grid_arrive_wait(&sync[0], ++barriers * unsigned(nwg), &err);
             const long long t2 = wall_clock64();
@@ -538,7 +558,10 @@ __global__ void __launch_bounds__(BR * G) k_jacobi_vt_blocks(const double* __res
             t_xch += (t1 - t0) + (wall_clock64() - t2);
         }
         // every workgroup reads the same flag (all were set before the last barrier of the sweep)
-        if (tid == 0) rotated = int(__hip_atomic_load(&sync[1 + sweep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (tid == 0) {
+            rotated = int(__hip_atomic_load(&sync[1 + sweep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (early && rotated) rotated = int(__hip_atomic_load(&sync[64 + sweep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
         __syncthreads();
         converged = rotated == 0;
         ++sweep;
@@ -598,21 +621,21 @@ namespace {
 // co-resident on any MI355X, which the grid barrier needs)
 template <int BR, int G, int E, bool ACC>
 void launch_blocks(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt, double* U,
-                   int ldu, int* status_dev, int max_sweeps, bool stamps = false) {
+                   int ldu, int* status_dev, int max_sweeps, bool stamps = false, bool early = false) {
     int nb = (p + BR - 1) / BR;
     nb += nb & 1;
-    const int sweeps = std::min(max_sweeps, SVB_SYNC_WORDS - 1);
+    const int sweeps = std::min(max_sweeps, 63);
     DevBuf slots(h, size_t(nb) * BR * E * G * 8), sync(h, SVB_SYNC_WORDS * 4), norms(h, size_t(p) * 8);
     XRS_HIP(hipMemsetAsync(sync.d(), 0, SVB_SYNC_WORDS * 4, h->stream));
     hipLaunchKernelGGL((k_jacobi_vt_blocks<BR, G, E, ACC>), dim3(nb / 2), dim3(BR * G), 0, h->stream, W, ldw, int(trans), p, q, nb, sweeps,
-                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev, stamps ? 1 : 0);
+                       slots.d(), sync.as<unsigned>(), norms.d(), S, Vt, ldvt, U, ldu, status_dev, (stamps ? 1 : 0) | (early ? 2 : 0));
     check_launch("k_jacobi_vt_blocks");
 }
 
 }  // namespace
 
 void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* S, double* Vt, int ldvt,
-               int* status_dev, int max_sweeps, int kernel, bool stamps) {
+               int* status_dev, int max_sweeps, int kernel, bool stamps, bool early) {
     XRS_REQUIRE(p >= 1 && p <= q && (p <= SV_MAXP || (q <= 2 * SVB_QMAX && kernel != 1)),
                 "jacobi_vt: need 1 <= p <= q, p <= 512 (one workgroup) or q <= 1024 (blocks)");
     XRS_REQUIRE(kernel >= 0 && kernel <= 2, "jacobi_vt: kernel is 0 (auto), 1 (one workgroup) or 2 (blocks)");
@@ -623,13 +646,13 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
     const bool blocks_ok = q <= 2 * SVB_QMAX;
     XRS_REQUIRE(kernel != 2 || blocks_ok, "jacobi_vt: the block kernel needs q <= 1024");
     if (q > SVB_QMAX) {   // rows of up to 1024 columns: blocks of 8 rows (2 x 8 x 1024 doubles of LDS)
-        launch_blocks<8, 32, 32, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
+        launch_blocks<8, 32, 32, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps, early);
     } else if (blocks_ok && (kernel == 2 || (kernel == 0 && p >= block_min))) {
         // register tiling E * 32 columns: the narrowest that holds q (padding costs FMAs and LDS traffic)
-        if (q <= 64) launch_blocks<16, 32, 2, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
-        else if (q <= 128) launch_blocks<16, 32, 4, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
-        else if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
-        else launch_blocks<16, 32, 16, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps);
+        if (q <= 64) launch_blocks<16, 32, 2, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps, early);
+        else if (q <= 128) launch_blocks<16, 32, 4, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps, early);
+        else if (q <= 256) launch_blocks<16, 32, 8, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps, early);
+        else launch_blocks<16, 32, 16, false>(h, W, ldw, trans, p, q, S, Vt, ldvt, nullptr, 0, status_dev, max_sweeps, stamps, early);
     } else if (jacobi_vt_fits_lds(p, q)) {
         hipLaunchKernelGGL(k_jacobi_vt_lds, dim3(1), dim3(SVL_THREADS), 0, h->stream, W, ldw, int(trans), p, q, max_sweeps, S, Vt,
                            ldvt, status_dev);
@@ -645,14 +668,14 @@ void jacobi_vt(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int 
 bool jacobi_usv_fits(int p, int q) { return p >= 1 && p <= q && 32 * ((q + 31) / 32) + p <= 1024; }
 
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
-                int* status_dev, int max_sweeps) {
+                int* status_dev, int max_sweeps, bool early) {
     XRS_REQUIRE(jacobi_usv_fits(p, q), "jacobi_usv: need p <= q and 32 ceil(q / 32) + p <= 1024");
     KernelTimer timer(h, XRS_KFAM_SVD, 3.5 * double(p) * p * (q + p) * 6.0, 16.0 * double(p) * (q + p));
     const int width = 32 * ((q + 31) / 32) + p;
-    if (width <= 128) launch_blocks<16, 32, 4, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
-    else if (width <= 256) launch_blocks<16, 32, 8, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
-    else if (width <= 512) launch_blocks<16, 32, 16, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
-    else launch_blocks<8, 32, 32, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps);
+    if (width <= 128) launch_blocks<16, 32, 4, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps, false, early);
+    else if (width <= 256) launch_blocks<16, 32, 8, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps, false, early);
+    else if (width <= 512) launch_blocks<16, 32, 16, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps, false, early);
+    else launch_blocks<8, 32, 32, true>(h, W, ldw, trans, p, q, S, Vt, ldvt, U, ldu, status_dev, max_sweeps, false, early);
 }
 
 int jacobi_settle(xrs_handle_t h, int* status_dev, int p, int q, const std::function<void(int kernel)>& rerun) {
@@ -679,13 +702,14 @@ int jacobi_settle(xrs_handle_t h, int* status_dev, int p, int q, const std::func
 // no division by S), and Jacobi on the columns of a triangular factor converges in about as many sweeps
 // for graded as for flat spectra (10-11 at g = 128; the rows of a lower factor of a graded matrix take
 // ~30). An upper factor (tall edge, B = Q R) already has the good orientation: rows of F.
-void jacobi_right_vectors(xrs_handle_t h, const double* F, int g, bool lower, double* S, double* Vt, int* status_dev, int max_sweeps) {
+void jacobi_right_vectors(xrs_handle_t h, const double* F, int g, bool lower, double* S, double* Vt, int* status_dev, int max_sweeps,
+                          bool early) {
     if (!lower || !jacobi_usv_fits(g, g)) {
-        jacobi_vt(h, F, g, false, g, g, S, Vt, g, status_dev, max_sweeps);
+        jacobi_vt(h, F, g, false, g, g, S, Vt, g, status_dev, max_sweeps, 0, false, early);
         return;
     }
     DevBuf J(h, size_t(g) * g * 8), Ul(h, size_t(g) * g * 8);
-    jacobi_usv(h, F, g, true, g, g, J.d(), g, S, Ul.d(), g, status_dev, max_sweeps);   // J.d()[i][j] = v_j[i]
+    jacobi_usv(h, F, g, true, g, g, J.d(), g, S, Ul.d(), g, status_dev, max_sweeps, early);   // J.d()[i][j] = v_j[i]
     transpose(h, Vt, J.d(), size_t(g), size_t(g));
 }
 

@@ -903,7 +903,8 @@ bool round_general(TT& t, const size_t* max_ranks, double eps) {
         // wide L through its columns with the rotations accumulated, tall R through its rows): accurate to u
         // whatever the singular value (no division by S), so the new core V_kk^T Q has orthonormal rows to
         // ~u even after eps cuts far below sqrt(u)
-        jacobi_right_vectors(h, F, int(gg), wide, S, V, js);
+        static const bool no_early = std::getenv("XRS_JACOBI_NO_EARLY") != nullptr;
+        jacobi_right_vectors(h, F, int(gg), wide, S, V, js, 40, !no_early);
         jac.push_back(int(k));
         hipLaunchKernelGGL(k_cut_rows, dim3(grid_for(gg * gg)), dim3(256), 0, h->stream, V, S, int(gg),
                            long(std::min<size_t>(max_ranks[k - 1], size_t(1) << 40)), eps, st + kRank + int(k));
