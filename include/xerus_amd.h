@@ -261,6 +261,12 @@ int xrs_comm_create(xrs_handle_t handle, int nranks, int rank, const void* id128
 int xrs_comm_destroy(xrs_comm_t comm);
 size_t xrs_comm_calls(xrs_comm_t comm);
 int xrs_comm_allreduce(void* comm, double* buf, size_t count);
+/** Emulated communicator for per-rank timing on one GPU (no RCCL): rank 0 of `nranks` ranks that hold
+ *  IDENTICAL mode slices, i.e. the sharding of the TT whose every mode is the local one repeated nranks
+ *  times. xrs_comm_allreduce on it enqueues buf *= nranks (exactly that TT's sum over ranks) on the handle's
+ *  stream; all-gather is refused. A diagnostic: the sharded round then runs a real rank's kernels, with
+ *  collectives of zero cost (tools/cfg5_rank_probe.py). */
+int xrs_comm_emulate(xrs_handle_t handle, int nranks, xrs_comm_t* comm_out);
 /** xrs_allgather_fn of the communicator: ncclAllGather (fp64) enqueued on the handle's stream. */
 int xrs_comm_allgather(void* comm, const double* send, double* recv, size_t count);
 

@@ -137,3 +137,34 @@ def test_sharded_sum_and_graded_rounds_world2():
 def test_sharded_small_sum_world3_uneven():
     out = _run(3, "small")
     _check(out, 3, unique=())
+
+
+def test_emulated_comm_rank0_of_replicated_tt(handle, ref):
+    """xrs_comm_emulate (the per-rank timing probe's communicator, tools/cfg5_rank_probe.py): rank 0 of 3
+    ranks holding identical slices equals the first m slices of the single-GPU round of the TT whose modes are
+    the local block repeated 3 times (the chain round and the truncating round)."""
+    from xerus_amd import capi
+    from xerus_amd import dist as xd
+
+    d, m, world = 6, 4, 3
+    ranks = bench.tt_ranks(d, m, 12)[1:-1]
+    x = ref.TT.random_raw([m] * d, ranks, ref.Rng(41))
+    full = [np.concatenate([c] * world, axis=1) for c in x.cores]
+    comm = xd.EmulatedComm(handle, world)
+    try:
+        for target in (12, 5):
+            st = xd.ShardedTT(handle, capi.TTDevice.from_cores(handle, x.cores), [m * world] * d, world, 0)
+            path = st.round_sharded(target, comm)
+            assert path in ("chain", "truncate"), path
+            g = capi.TTDevice.from_cores(handle, full)
+            g.round(target)
+            assert st.ranks == g.ranks
+            # the represented tensors on rank 0's index block (the cores' gauge may differ by signs)
+            a = ref.TT(st.local.cores()).full()
+            b = ref.TT([c[:, :m, :] for c in g.cores()]).full()
+            assert np.linalg.norm(a - b) <= 1e-10 * np.linalg.norm(b), (target, np.linalg.norm(a - b) / np.linalg.norm(b))
+            st.local.free()
+            g.free()
+        assert comm.calls > 0
+    finally:
+        comm.close()

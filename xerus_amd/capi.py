@@ -81,6 +81,7 @@ SIGNATURES = {
                                         C.POINTER(C.c_double)]),
     "xrs_comm_unique_id": (C.c_int, [_DP]),
     "xrs_comm_create": (C.c_int, [_DP, C.c_int, C.c_int, _DP, C.POINTER(_DP)]),
+    "xrs_comm_emulate": (C.c_int, [_DP, C.c_int, C.POINTER(_DP)]),
     "xrs_comm_destroy": (C.c_int, [_DP]),
     "xrs_comm_calls": (_SZ, [_DP]),
     "xrs_comm_allreduce": (C.c_int, [_DP, _DP, _SZ]),

@@ -11,6 +11,7 @@
 
 #include <cstring>
 
+#include "elementwise.hpp"
 #include "runtime.hpp"
 
 struct xrs_comm_s {
@@ -18,6 +19,7 @@ struct xrs_comm_s {
     xrs_handle_t h = nullptr;
     int nranks = 1, rank = 0;
     size_t calls = 0, bytes = 0;
+    bool emulated = false;   // xrs_comm_emulate: no RCCL; the sum over ranks is nranks x the local value
 };
 
 namespace xrs {
@@ -101,6 +103,18 @@ int xrs_comm_create(xrs_handle_t h, int nranks, int rank, const void* id, xrs_co
     });
 }
 
+int xrs_comm_emulate(xrs_handle_t h, int nranks, xrs_comm_t* out) {
+    return guarded([&] {
+        XRS_REQUIRE(h && out, "null argument");
+        XRS_REQUIRE(nranks >= 1, "invalid world size");
+        auto* c = new xrs_comm_s;
+        c->h = h;
+        c->nranks = nranks;
+        c->emulated = true;
+        *out = c;
+    });
+}
+
 int xrs_comm_destroy(xrs_comm_t c) {
     return guarded([&] {
         if (!c) return;
@@ -113,16 +127,24 @@ size_t xrs_comm_calls(xrs_comm_t c) { return c ? c->calls : 0; }
 
 int xrs_comm_allreduce(void* ctx, double* buf, size_t count) {
     auto* c = static_cast<xrs_comm_s*>(ctx);
-    if (!c || !c->comm || (count && !buf)) return 1;
+    if (!c || !(c->comm || c->emulated) || (count && !buf)) return 1;
     ++c->calls;
     c->bytes += count * 8;
     if (count == 0) return 0;
+    if (c->emulated) {   // nranks identical slices: the sum is nranks x the local value, in stream order
+        try {
+            xrs::scal(c->h, buf, double(c->nranks), count);
+        } catch (...) {
+            return 1;
+        }
+        return 0;
+    }
     return rccl().all_reduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->h->stream) == ncclSuccess ? 0 : 1;
 }
 
 int xrs_comm_allgather(void* ctx, const double* send, double* recv, size_t count) {
     auto* c = static_cast<xrs_comm_s*>(ctx);
-    if (!c || !c->comm || (count && !(send && recv))) return 1;
+    if (!c || !c->comm || c->emulated || (count && !(send && recv))) return 1;
     ++c->calls;
     c->bytes += count * 8 * size_t(c->nranks);
     if (count == 0) return 0;

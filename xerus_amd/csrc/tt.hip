@@ -240,8 +240,9 @@ void right_gram_step(TT& t, std::vector<double*>& H, double* T, size_t k, bool d
 // Both chains (G: left Grams, only with `left`; H: right Grams; `store` owns the memory). Unsharded,
 // concurrently (left on a side stream, right on the main stream) with their launches interleaved step by
 // step. (Both chains' products as one two-entry grid on one stream measured slower: one chain's split-K
-// reduce and boundary products no longer overlap the other chain's GEMMs) Sharded, step s of both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s}
-// sit side by side in one buffer.
+// reduce and boundary products no longer overlap the other chain's GEMMs) Sharded, step s of
+// both chains shares ONE all-reduce: G_{s+1} and H_{d-1-s} sit side by side in one buffer, the two steps
+// forked onto two streams and joined before it.
 void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::vector<DevBuf>& store, bool left) {
     const size_t d = t.d;
     xrs_handle_t h = t.h;
@@ -258,8 +259,16 @@ void gram_chains(TT& t, std::vector<double*>& G, std::vector<double*>& H, std::v
             double* base = store.back().d();
             if (left) G[kl] = base;
             H[kr] = base + nl;
-            if (left) left_gram_step(t, G, TL.d(), s, false);
-            right_gram_step(t, H, TR.d(), kr, false);
+            if (left) {   // the two chains' steps concurrently (left on a side stream), joined before the all-reduce
+                StreamFork fork(h);
+                fork.side();
+                left_gram_step(t, G, TL.d(), s, false);
+                fork.main();
+                right_gram_step(t, H, TR.d(), kr, false);
+                fork.join();
+            } else {
+                right_gram_step(t, H, TR.d(), kr, false);
+            }
             t.reduce(base, nl + nr);
         }
         return;

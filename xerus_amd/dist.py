@@ -175,6 +175,18 @@ class RcclComm:
             pass
 
 
+class EmulatedComm(RcclComm):
+    """xrs_comm_emulate: rank 0 of `world` ranks holding identical slices (the sum over ranks is `world` x the
+    local value, enqueued on the stream). Per-rank timing of the sharded path on one GPU; not a collective."""
+
+    def __init__(self, handle: capi.Handle, world: int):
+        self.handle, self.lib = handle, handle.lib
+        self.comm = C.c_void_p()
+        capi._check("xrs_comm_emulate", self.lib.xrs_comm_emulate(handle.h, world, C.byref(self.comm)))
+        self.world, self.rank = world, 0
+        self.device_native = True
+
+
 class ShardedTT:
     """This rank's mode slices of a TT (capi.TTDevice over the local slices) + the global mode sizes."""
 
