@@ -713,9 +713,11 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
     const int ksteps = (K + bk - 1) / bk;
     int splits = g_env.second;
     if (splits <= 0) {
-        // split-K toward ~256 workgroups with >= 4 K-steps of 32 per slice
+        // split-K toward ~256 workgroups (XRS_SG_TARGET: another count, tuning) with >= 4 K-steps of 32 per slice
+        int target = 256;
+        if (const char* e = std::getenv("XRS_SG_TARGET")) target = std::max(1, std::atoi(e));
         splits = 1;
-        if (tiles < 192) splits = std::max(1, std::min((256 + tiles - 1) / tiles, ksteps * bk / 128));
+        if (tiles < 192) splits = std::max(1, std::min((target + tiles - 1) / tiles, ksteps * bk / 128));
     }
     splits = std::max(1, std::min(splits, ksteps));
     const int kps = (ksteps + splits - 1) / splits * bk;
