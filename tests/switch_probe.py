@@ -29,6 +29,15 @@ def main():
         E = A @ B
         errs.append(float(np.abs(dC.numpy() - E).max() / np.abs(E).max()))
     out["gemm_err"] = max(errs)
+    # fp32 split-K product (xrs_gemm_f32; XRS_SG_TARGET moves its slice count)
+    A32 = rng.standard_normal((5120, 256)).astype(np.float32)
+    B32 = rng.standard_normal((5120, 256)).astype(np.float32)
+    dA, dB, dC = h.array_f32(A32), h.array_f32(B32), capi.Float32Array(h, (256, 256))
+    h.gemm_f32(dC, 256, 256, 1.0, dA, 256, True, 5120, dB, 256, False)
+    E = A32.astype(np.float64).T @ B32.astype(np.float64)
+    out["sgemm_err"] = float(np.linalg.norm(dC.numpy() - E) / np.linalg.norm(E))
+    for d in (dA, dB, dC):
+        d.free()
     # <x,y> synchronous and asynchronous (the gate)
     dims, ranks = [10] * 6, [10, 40, 40, 40, 10]
     x = ref.TT.random_raw(dims, ranks, ref.Rng(3))

@@ -1,4 +1,4 @@
-"""Every XRS_* environment switch the library reads (DESIGN.md §8), each run in a subprocess
+"""Every XRS_* environment switch the library reads (DESIGN.md §5), each run in a subprocess
 (tests/switch_probe.py: the switches are read once per process): results stay within the parity bars and
 each switch has its documented effect (path taken, diagnostics printed)."""
 import json
@@ -28,6 +28,7 @@ def _probe(env):
 
 def _bars(r):
     assert r["gemm_err"] <= 1e-13
+    assert r["sgemm_err"] <= 1e-6
     assert r["dot_err"] <= 1e-12 and r["dot_async_err"] <= 1e-12
     assert r["chain_path"] == "chain" and r["chain_err"] <= 1e-10
     assert r["trunc_ranks_ok"] and r["trunc_err_diff"] <= 1e-6
@@ -46,8 +47,12 @@ def _bars(r):
     ({"XRS_DEBUG_ROUND": "1"}, lambda r, err: "round_truncate:" in err and "round_general:" in err),
     ({"XRS_STAMPS": "all"}, lambda r, err: "[round host us]" in err and "jacobi_vt p=" in err and "k_sytrd n=" in err),
     ({"XRS_SYNC_DEBUG": "1"}, lambda r, err: "[xrs] launched k_gemm" in err),
+    ({"XRS_JACOBI_NO_EARLY": "1"}, lambda r, err: r["graded_path"] == "general"),     # confirming Jacobi sweep
+    ({"XRS_GLDS_ST2": "1"}, lambda r, err: True),                                      # 2-stage LDS-DMA tiles
+    ({"XRS_SG_TARGET": "96"}, lambda r, err: True),                                    # fp32 split-K target
+    ({"XRS_SGEMM": "1,8"}, lambda r, err: True),                                       # forced fp32 tile / split
 ], ids=["default", "dot_gate", "gemm_glds", "gemm_cfg", "no_general", "trunc_jacobi", "syev_max", "debug_round",
-        "stamps", "sync_debug"])
+        "stamps", "sync_debug", "jacobi_no_early", "glds_st2", "sg_target", "sgemm"])
 def test_switch(env, check):
     r, err = _probe(env)
     _bars(r)
