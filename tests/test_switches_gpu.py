@@ -48,7 +48,7 @@ def _bars(r):
     ({"XRS_STAMPS": "all"}, lambda r, err: "[round host us]" in err and "jacobi_vt p=" in err and "k_sytrd n=" in err),
     ({"XRS_SYNC_DEBUG": "1"}, lambda r, err: "[xrs] launched k_gemm" in err),
     ({"XRS_JACOBI_NO_EARLY": "1"}, lambda r, err: r["graded_path"] == "general"),     # confirming Jacobi sweep
-    ({"XRS_GLDS_ST2": "1"}, lambda r, err: True),                                      # 2-stage LDS-DMA tiles
+    ({"XRS_GLDS_ST2": "0"}, lambda r, err: True),                                      # 3-stage LDS-DMA tiles
     ({"XRS_SG_TARGET": "96"}, lambda r, err: True),                                    # fp32 split-K target
     ({"XRS_SGEMM": "1,8"}, lambda r, err: True),                                       # forced fp32 tile / split
 ], ids=["default", "dot_gate", "gemm_glds", "gemm_cfg", "no_general", "trunc_jacobi", "syev_max", "debug_round",

@@ -742,11 +742,15 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         return std::make_pair(v, t);
     }();
     const int g_var = g_env.first, g_target = g_env.second;
-    // XRS_GLDS_ST2=1 (A/B): the 8-wave tiles (g4 / g6 / g7) with 2 LDS stages of 32-deep K-steps (64-74 KB:
-    // two workgroups per CU) instead of 3 (96-110 KB: one)
-    static const bool g_st2 = [] {
+    // The 8-wave tiles run with 2 LDS stages of 32-deep K-steps (64-74 KB: two workgroups per CU) instead of
+    // 3 (96-110 KB: one), while the split-K choice still counts one workgroup per CU: the concurrent lanes of
+    // a round (both Gram chains, <x,y> beside the round) then share every CU, one workgroup's barrier /
+    // fragment-read bubbles filled by the other's MFMAs (bench step 1.10 -> 1.00 ms, r05y; alone the TT-shape
+    // GEMMs are unchanged within 3 %). XRS_GLDS_ST2=mask (A/B): bit 0 the products (g6 / g7), bit 1 the Grams
+    // (g4), bit 2 the one-workgroup split-K rule; default 7, 0 = the 3-stage tiles.
+    static const int g_st2 = [] {
         const char* e = std::getenv("XRS_GLDS_ST2");
-        return e && e[0] == '1';
+        return e ? std::atoi(e) : 7;
     }();
     if (g_var == 0) return false;
     if (K % kGldsBK != 0 || (lda & 1) || (ldb & 1)) return false;
@@ -789,7 +793,8 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         // second, mostly idle round (the 6 orthogonality Grams of the bench round: 60 tiles x 5 slices =
         // 300 workgroups on 256 CUs, 64 K-steps per CU, against 40 at 4 slices).
         const int nwaves = (var == 4 || var == 6 || var == 7) ? 8 : 4;
-        const int nst = (bk == 64 || (g_st2 && nwaves == 8)) ? 2 : 3;
+        const bool st2 = (var == 4 && (g_st2 & 2)) || ((var == 6 || var == 7) && (g_st2 & 1));
+        const int nst = (bk == 64 || (st2 && !(g_st2 & 4))) ? 2 : 3;
         const int lds_kb = nst * (bms[var] + bns[var]) * bk * 8 / 1024;
         const long resident = long(g_target) * std::max(1, std::min(160 / lds_kb, 16 / nwaves));
         const int smax = std::max(1, ksteps * bk / 128);
@@ -812,9 +817,9 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         case 1: XRS_GLDS(64, 80, 4, 1, 1); break;
         case 2: XRS_GLDS(80, 64, 1, 4, 1); break;
         case 3: XRS_GLDS(64, 64, 2, 2, 1); break;
-        case 4: if (g_st2) XRS_GLDS(64, 64, 2, 2, 2, kGldsBK, 2); else XRS_GLDS(64, 64, 2, 2, 2); break;
-        case 6: if (g_st2) XRS_GLDS(64, 80, 4, 1, 2, kGldsBK, 2); else XRS_GLDS(64, 80, 4, 1, 2); break;
-        case 7: if (g_st2) XRS_GLDS(80, 64, 1, 4, 2, kGldsBK, 2); else XRS_GLDS(80, 64, 1, 4, 2); break;
+        case 4: if (g_st2 & 2) XRS_GLDS(64, 64, 2, 2, 2, kGldsBK, 2); else XRS_GLDS(64, 64, 2, 2, 2); break;
+        case 6: if (g_st2 & 1) XRS_GLDS(64, 80, 4, 1, 2, kGldsBK, 2); else XRS_GLDS(64, 80, 4, 1, 2); break;
+        case 7: if (g_st2 & 1) XRS_GLDS(80, 64, 1, 4, 2, kGldsBK, 2); else XRS_GLDS(80, 64, 1, 4, 2); break;
         case 8: XRS_GLDS(64, 80, 2, 1, 2); break;
         case 9: XRS_GLDS(80, 64, 1, 2, 2); break;
         case 10: XRS_GLDS(64, 64, 1, 1, 4); break;
