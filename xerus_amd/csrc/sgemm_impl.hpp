@@ -253,8 +253,11 @@ __device__ __forceinline__ void block_max_atomic(unsigned* w, float m, float* re
 // buffer and issues the loads of step t+PD into slot t % PD; one barrier per step. PD = 4 keeps twice the
 // bytes in flight of PD = 2: short-K slices (the environment products' 10 steps) are load-latency bound. (A 3-stage LDS ring whose last chunk read
 // the next step's first fragments ahead of the barrier measured slower on every shape: DESIGN.md §3.6.)
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, int ST, bool TA, bool TB, class EA, class EB, int MODE>
-__global__ void __launch_bounds__(WGM * WGN * WGK * 64) k_sgemm(const Args p) {
+// OCC: minimum waves per SIMD (the second __launch_bounds__ argument): 4 caps the registers at 128 per lane so that two
+// 8-wave workgroups share a CU (the concurrent zipper ends: cfg 13; the 64x80 / 80x64 forms 14 / 15 spill at 128)
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, int ST, bool TA, bool TB, class EA, class EB, int MODE,
+          int OCC = 1>
+__global__ void __launch_bounds__(WGM * WGN * WGK * 64, OCC) k_sgemm(const Args p) {
     static_assert(ST == 2 || ST == 3, "2 or 3 LDS stages");
     constexpr bool VEC = MODE >= 1, WHOLE = MODE == 2;
     // fp32-only products carry no operand scales (the fp32 zipper's mixed products always do)
@@ -641,17 +644,18 @@ struct Cfg {
 // only (XRS_SGEMM, fp32 operands): 5 64x64 with 64-deep K-steps, 6 / 7 / 9 the 64x64 / 64x80 / 80x64 tiles with a
 // 2-step ring, 8 128x128 with 3 LDS stages, 10 / 11 / 12 the 64x64 / 64x80 / 80x64 tiles with 3 LDS stages (the next
 // step's first fragments read ahead of the barrier)
-constexpr int kNumCfgs = 13;
+constexpr int kNumCfgs = 16;
 constexpr Cfg kCfgs[kNumCfgs] = {{128, 128, 32}, {64, 64, 32}, {64, 80, 32}, {80, 64, 32}, {32, 32, 32},
                                  {64, 64, 64},   {64, 64, 32}, {64, 80, 32}, {128, 128, 32}, {80, 64, 32},
-                                 {64, 64, 32},   {64, 80, 32}, {80, 64, 32}};
+                                 {64, 64, 32},   {64, 80, 32}, {80, 64, 32}, {64, 64, 32},   {64, 80, 32},
+                                 {80, 64, 32}};
 
-template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, int ST, class EA, class EB>
+template <int BM, int BN, int WGM, int WGN, int WGK, int BK, int PD, int ST, class EA, class EB, int OCC = 1>
 void launch_cfg(xrs_handle_t h, const Args& p, bool ta, bool tb, int mode, int tiles, int splits, double bytes) {
     const dim3 grid(unsigned(tiles), 1u, unsigned(splits));
     KernelTimer timer(h, XRS_KFAM_GEMM, 2.0 * double(p.M) * double(p.N) * double(p.K), bytes, true);
 #define XRS_SG(TA_, TB_, MODE_)                                                                                    \
-    hipExtLaunchKernelGGL((k_sgemm<BM, BN, WGM, WGN, WGK, BK, PD, ST, TA_, TB_, EA, EB, MODE_>), grid, dim3(WGM * WGN * WGK * 64), \
+    hipExtLaunchKernelGGL((k_sgemm<BM, BN, WGM, WGN, WGK, BK, PD, ST, TA_, TB_, EA, EB, MODE_, OCC>), grid, dim3(WGM * WGN * WGK * 64), \
                           0, h->stream, timer.start(), timer.stop(), 0, p)
 #define XRS_SG_FLAGS(MODE_)                                  \
     if (!ta && !tb) XRS_SG(false, false, MODE_);              \
@@ -697,12 +701,16 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
     auto tiles_of = [&](int c) { return ((M + kCfgs[c].bm - 1) / kCfgs[c].bm) * ((N + kCfgs[c].bn - 1) / kCfgs[c].bn); };
     constexpr bool kTune = std::is_same<EA, float>::value && std::is_same<EB, float>::value;
     int cfg = g_env.first;
-    if (cfg < 0 || cfg >= (kTune ? kNumCfgs : 5)) {
+    if (cfg < 0 || cfg >= kNumCfgs || (!kTune && cfg >= 5 && cfg < 13)) {
         if (tiles_of(0) >= 200) cfg = 0;
         else if (M % 64 == 0 && N % 80 == 0 && tiles_of(2) >= 192 && tiles_of(2) <= 320) cfg = 2;
         else if (M % 80 == 0 && N % 64 == 0 && tiles_of(3) >= 192 && tiles_of(3) <= 320) cfg = 3;
         else if (M >= 48 && N >= 48) cfg = 1;
         else cfg = 4;
+        // an fp64 operand (the zipper's cores): the 64x64 tile with a 2-step ring capped at 128 registers, so
+        // two workgroups share a CU -- the two zipper ends' launches run concurrently (dot_f32 0.25 -> 0.224 ms,
+        // profiles/r05/dot32_occ4_ab_r05aa.txt); the fp32 x fp32 64x64 kernel already fits 120 registers
+        if (!kTune && cfg >= 1 && cfg <= 3) cfg = 13;
     }
     const int bk = kCfgs[cfg].bk, bm = kCfgs[cfg].bm, bn = kCfgs[cfg].bn;
     const int tiles = tiles_of(cfg);
@@ -738,12 +746,16 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
            unsigned(slab_bytes), splits > 1 ? h->tickets : nullptr, (M + kCfgs[cfg].bm - 1) / kCfgs[cfg].bm, xg};
     const double bytes = double(sizeof(EA)) * M * K + double(sizeof(EB)) * K * N + 4.0 * M * N * (splits > 1 ? 2 * splits : 1);
 #define XRS_CFG(...) launch_cfg<__VA_ARGS__, EA, EB>(h, p, ta, tb, mode, tiles, splits, bytes)
+#define XRS_CFG4(...) launch_cfg<__VA_ARGS__, EA, EB, 4>(h, p, ta, tb, mode, tiles, splits, bytes)
     switch (cfg) {
         case 0: XRS_CFG(128, 128, 2, 4, 1, 32, 2, 2); break;
         case 1: XRS_CFG(64, 64, 2, 2, 2, 32, 4, 2); break;
         case 2: XRS_CFG(64, 80, 4, 1, 2, 32, 4, 2); break;
         case 3: XRS_CFG(80, 64, 1, 4, 2, 32, 4, 2); break;
         case 4: XRS_CFG(32, 32, 2, 1, 1, 32, 2, 2); break;
+        case 13: XRS_CFG4(64, 64, 2, 2, 2, 32, 2, 2); break;
+        case 14: XRS_CFG4(64, 80, 4, 1, 2, 32, 2, 2); break;
+        case 15: XRS_CFG4(80, 64, 1, 4, 2, 32, 2, 2); break;
         default:
             if constexpr (kTune) {
                 switch (cfg) {
@@ -760,6 +772,7 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
             break;
     }
 #undef XRS_CFG
+#undef XRS_CFG4
 }
 
 }  // namespace xrs
