@@ -299,7 +299,7 @@ int xrs_tt_round_sharded(xrs_handle_t handle, size_t d, const size_t* n_local, s
  *  structural-excess QC steps at the left end -- are gathered by one all-reduce of a zero-padded core
  *  (small: bounded by r^2) and factorised replicated. *path = XRS_ROUND_CHAIN / _TRUNCATE / _GENERAL on
  *  success, 0 if every certificate failed (then the left-end QC steps may have been applied: the cores
- *  represent the same tensor; gather and use xrs_tt_round). world * d <= 2048. */
+ *  represent the same tensor; gather and use xrs_tt_round). world * d <= 2040. */
 int xrs_tt_round_sharded_ex(xrs_handle_t handle, size_t d, const size_t* n_local, size_t* r, double** cores,
                             const size_t* max_ranks, double eps, int world, int rank, xrs_allreduce_fn allreduce,
                             void* ctx, int* path);

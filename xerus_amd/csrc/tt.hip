@@ -1296,7 +1296,7 @@ int xrs_tt_round_sharded_ex(xrs_handle_t h, size_t d, const size_t* n_local, siz
         XRS_REQUIRE(d >= 2 && n_local && r && cores && max_ranks, "null TT description");
         XRS_REQUIRE(r[0] == 1 && r[d] == 1, "boundary ranks must be 1");
         XRS_REQUIRE(world >= 1 && rank >= 0 && rank < world, "world / rank out of range");
-        XRS_REQUIRE(size_t(world) * d <= 2048, "world * d above 2048");
+        XRS_REQUIRE(size_t(world) * d <= 2040, "world * d above 2040");
         XRS_REQUIRE(eps < 1.0 && eps >= 0.0, "_eps must be smaller than one.");
         for (size_t k = 0; k + 1 < d; ++k)
             XRS_REQUIRE(max_ranks[k] > 0, "Trying to round a TTTensor to rank 0 is not possible.");

@@ -243,8 +243,10 @@ ShardLayout shard_layout(TT& t) {
     if (!t.sharded()) return lay;
     xrs_handle_t h = t.h;
     const size_t w = t.world > 0 ? size_t(t.world) : 1, me = t.world > 0 ? size_t(t.rank) : 0;
-    XRS_REQUIRE(w * d <= 2048 && me < w, "shard_layout: world / rank out of range");
-    double* hn = static_cast<double*>(h->host_scratch) + 3400;   // (pinned scratch: doubles 3400 .. 5448)
+    XRS_REQUIRE(w * d <= 2040 && me < w, "shard_layout: world / rank out of range");
+    // (pinned scratch: doubles 4100 .. 6140, a region no other routine uses -- 2048.. the check points'
+    // deviations, 4096 dot_two_ended's unit environments, 6144.. the status words)
+    double* hn = static_cast<double*>(h->host_scratch) + 4100;
     for (size_t i = 0; i < w * d; ++i) hn[i] = 0.0;
     for (size_t k = 0; k < d; ++k) hn[me * d + k] = double(t.n[k]);
     DevBuf tab(h, w * d * 8);
