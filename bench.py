@@ -79,7 +79,7 @@ def random_cores(xe, dims, ranks, seed):
 
 def load_traffic():
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC pass of this bench (or None)."""
-    for tag in ("r04", "r03", "r02"):   # the newest committed pass
+    for tag in ("r05", "r04", "r03", "r02"):   # the newest committed pass
         p = os.path.join(ROOT, "profiles", tag, "pmc_traffic.json")
         if os.path.exists(p):
             break
