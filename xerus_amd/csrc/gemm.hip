@@ -97,14 +97,16 @@ k_gemm_f64(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps,
 // Accumulators -> C: sums the NACC accumulator sets, reduces the WGK wave groups through LDS (`lds`, at
 // least (WGK-1) * WGM * WGN * TM * TN * 256 doubles, free to overwrite), then stores C (alpha, symmetric
 // mirror), a split-K slab, or a slab + the in-launch combine (tickets). Shared by both GEMM kernels.
+// xb / yb / zb: the workgroup's tile index, batch entry and split-K slice (blockIdx.x / .y / .z, or the
+// XCD-grouped mapping of k_gemm_glds)
 template <int TM, int TN, int WGM, int WGN, int WGK, int NACC, class PTR>
 __device__ __forceinline__ void gemm_finish(d4 (&acc2)[NACC][TM][TN], double* lds, const PTR& ptrs, int M, int N,
                                             double alpha, double* __restrict__ slab, int* __restrict__ tickets,
-                                            int sym, int m0, int n0, int wm, int wn, int kg, int pos) {
-    const int bz = blockIdx.y;
+                                            int sym, int m0, int n0, int wm, int wn, int kg, int pos, int xb, int yb, int zb) {
+    const int bz = yb;
     double* __restrict__ C = ptrs.c(bz);
-    const int zslice = bz * int(gridDim.z) + int(blockIdx.z);
-    const int tslot = bz * int(gridDim.x) + int(blockIdx.x);
+    const int zslice = bz * int(gridDim.z) + zb;
+    const int tslot = bz * int(gridDim.x) + xb;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const bool mirror = sym != 0;
@@ -399,7 +401,8 @@ __device__ __forceinline__ void gemm_body(const PTR& ptrs, size_t lda, size_t ld
         }
     }
 
-    gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, &As[0][0], ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
+    gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, &As[0][0], ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos,
+                                             int(blockIdx.x), int(blockIdx.y), int(blockIdx.z));
 }
 
 // ---------------------------------------------------------------------------------------------------
@@ -501,7 +504,20 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
     constexpr int NACC = (TM * TN <= 2) ? 2 : 1;
     static_assert(WGK == 1 || (WGK - 1) * WGM * WGN * TM * TN * 256 <= S * STAGE, "LDS reduction buffer too small");
 
-    const int bz = blockIdx.y;
+    // tile index xb, batch entry bz and split-K slice zb. xcd_group 3 (split-K grids whose entry x slice
+    // count is a multiple of 8): workgroups are dealt to the 8 XCDs round-robin by dispatch order, so the
+    // linear id's residue picks the XCD and every XCD takes whole (entry, slice) pairs -- all tiles of one
+    // pair on one XCD: a slice's operand panels are fetched into ONE XCD's L2 instead of all eight (the
+    // step's Grams: 56 -> 41 MB of HBM reads per launch, profiles/r05/xcd_split_ab_r05ai.txt)
+    int xb = int(blockIdx.x), bz = int(blockIdx.y), zb = int(blockIdx.z);
+    if (xcd_group == 3) {
+        const int X = int(gridDim.x), Y = int(gridDim.y);
+        const int L = xb + X * (bz + Y * zb), c = L & 7, q = L >> 3;
+        const int u = c + 8 * (q / X);   // (entry, slice) pair
+        xb = q % X;
+        bz = u % Y;
+        zb = u / Y;
+    }
     const double* __restrict__ A = ptrs.a(bz);
     const double* __restrict__ B = ptrs.b(bz);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -509,13 +525,13 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
     const int wm = (pos / WGN) * WM, wn = (pos % WGN) * WN;
     int tm, tn;
     if (sym) {   // the grid holds the lower tiles only: x -> (tm, tn), tm >= tn, row by row
-        const int x = blockIdx.x;
+        const int x = xb;
         tm = int((__builtin_sqrtf(8.0f * float(x) + 1.0f) - 1.0f) * 0.5f);
         while ((tm + 1) * (tm + 2) / 2 <= x) ++tm;
         while (tm * (tm + 1) / 2 > x) --tm;
         tn = x - tm * (tm + 1) / 2;
     } else {
-        const int b = blockIdx.x, tiles_n = gridDim.x / tiles_m;
+        const int b = xb, tiles_n = gridDim.x / tiles_m;
         if (xcd_group == 1) {
             const int xcd = b & 7, slot = b >> 3;
             tn = (slot / tiles_m) * 8 + xcd;
@@ -534,8 +550,8 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
     // op(B) lower (bit 1) k >= n0 only -- whole K-steps of the slice's range
     const int klo = (tri & 2) ? (n0 / BK) * BK : 0;
     const int khi = (tri & 1) ? min(K, (m0 + BM + BK - 1) / BK * BK) : K;
-    const int kbeg = max(int(blockIdx.z) * kps, klo);
-    const int nsteps = max(0, min(khi, int(blockIdx.z) * kps + kps) - kbeg) / BK;   // (the host guarantees whole steps)
+    const int kbeg = max(zb * kps, klo);
+    const int nsteps = max(0, min(khi, zb * kps + kps) - kbeg) / BK;   // (the host guarantees whole steps)
     const bool full = wave < INSTR % NW || INSTR % NW == 0;     // issues PER_WAVE DMAs per stage (else one fewer)
 
     // this wave's DMA instructions: j = wave + NW u; j < IA::INSTR -> A image, else B image
@@ -624,7 +640,7 @@ __device__ __forceinline__ void glds_body(double* __restrict__ lds, const PTR& p
         }
     }
     __syncthreads();   // every wave is done with the stages before the epilogue reuses the LDS
-    gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, lds, ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos);
+    gemm_finish<TM, TN, WGM, WGN, WGK, NACC>(acc2, lds, ptrs, M, N, alpha, slab, tickets, sym, m0, n0, wm, wn, kg, pos, xb, bz, zb);
 }
 
 template <int BM, int BN, int WGM, int WGN, int WGK, bool TA, bool TB, class PTR, int BK = kGldsBK, int ST = 0>
@@ -700,6 +716,12 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
+    // XRS_GLDS_XCD_SPLIT=0 (A/B): the plain slice order
+    static const bool xcd_split = [] {
+        const char* e = std::getenv("XRS_GLDS_XCD_SPLIT");
+        return !(e && e[0] == '0');
+    }();
+    if (xcd_split && splits >= 2 && (count * splits) % 8 == 0) xg = 3;   // whole (entry, split-K slice) pairs per XCD
     // executed K-depth summed over the tile rows / columns (triangular operands skip their zero blocks)
     double kdepth = double(K);
     if (tri & 1) {
