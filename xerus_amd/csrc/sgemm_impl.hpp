@@ -279,9 +279,18 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64, OCC) k_sgemm(const Args 
     const EA* __restrict__ A = static_cast<const EA*>(p.A);
     const EB* __restrict__ B = static_cast<const EB*>(p.B);
 
+    // tile bx and split-K slice bz: xcd 3 (split-K grids whose slice count is a multiple of 8) deals whole
+    // slices to the XCDs (workgroups go to the 8 XCDs round-robin by dispatch order): a slice's operand
+    // panels are fetched into one XCD's L2 instead of all eight
+    int bx = int(blockIdx.x), bz = int(blockIdx.z);
+    if (p.xcd == 3) {
+        const int X = int(gridDim.x), L = bx + X * bz, c = L & 7, q = L >> 3;
+        bz = c + 8 * (q / X);
+        bx = q % X;
+    }
     int tm, tn;
     {
-        const int b = blockIdx.x, tiles_n = int(gridDim.x) / p.tiles_m;
+        const int b = bx, tiles_n = int(gridDim.x) / p.tiles_m;
         if (p.xcd == 1) {
             const int xcd = b & 7, slot = b >> 3;
             tn = (slot / p.tiles_m) * 8 + xcd;
@@ -297,7 +306,7 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64, OCC) k_sgemm(const Args 
     }
     XRS_SG_STAMP(0)
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kbeg = int(blockIdx.z) * p.kps, kend = min(p.K, kbeg + p.kps);
+    const int kbeg = bz * p.kps, kend = min(p.K, kbeg + p.kps);
     const int nsteps = (kend - kbeg + BK - 1) / BK;   // >= 1: the host launches non-empty slices only
     const float fa = p.sa ? pow2_scale(max_word(p.sa)) : 1.0f, fb = p.sb ? pow2_scale(max_word(p.sb)) : 1.0f;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -536,21 +545,21 @@ __global__ void __launch_bounds__(WGM * WGN * WGK * 64, OCC) k_sgemm(const Args 
     static_assert(WGM * WGN * TM * TN * 256 == BM * BN, "accumulator layout covers the tile");
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(p.slab, 0, int(p.slab_bytes), 0x00020000);
     auto soff = [&](int z, int i, int j) {
-        return int(((size_t(z) * gridDim.x + blockIdx.x) * (BM * BN) + size_t(((pos * TM + i) * TN + j) * 64 + lane) * 4) * 4);
+        return int(((size_t(z) * gridDim.x + bx) * (BM * BN) + size_t(((pos * TM + i) * TN + j) * 64 + lane) * 4) * 4);
     };
     if (kg == 0) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rs, soff(blockIdx.z, i, j), 0, 16);
+            for (int j = 0; j < TN; ++j) __builtin_amdgcn_raw_buffer_store_b128(acc[i][j], rs, soff(bz, i, j), 0, 16);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float* flag = lds;   // the one LDS array (no second __shared__ object)
     if (tid == 0) {
-        const int tk = __hip_atomic_fetch_add(&p.tickets[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int tk = __hip_atomic_fetch_add(&p.tickets[bx], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool last = (tk == int(gridDim.z) - 1);
-        if (last) __hip_atomic_store(&p.tickets[blockIdx.x], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) __hip_atomic_store(&p.tickets[bx], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag[0] = last ? 1.0f : 0.0f;
     }
     __syncthreads();
@@ -711,6 +720,9 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
         // two workgroups share a CU -- the two zipper ends' launches run concurrently (dot_f32 0.25 -> 0.224 ms,
         // profiles/r05/dot32_occ4_ab_r05aa.txt); the fp32 x fp32 64x64 kernel already fits 120 registers
         if (!kTune && cfg >= 1 && cfg <= 3) cfg = 13;
+        // fp32 x fp32 64x64: the 2-step ring (103 registers) measured 1-3 % faster than the 4-step one on
+        // 1024^3 (profiles/r05/sgemm_probe_r05ag.txt, r05j)
+        if (kTune && cfg == 1) cfg = 6;
     }
     const int bk = kCfgs[cfg].bk, bm = kCfgs[cfg].bm, bn = kCfgs[cfg].bn;
     const int tiles = tiles_of(cfg);
@@ -735,6 +747,11 @@ void sgemm(xrs_handle_t h, float* C, size_t Ms, size_t Ns, float alpha, const EA
         const int tm = (M + kCfgs[cfg].bm - 1) / kCfgs[cfg].bm, tn = (N + kCfgs[cfg].bn - 1) / kCfgs[cfg].bn;
         if (double(N) >= double(M)) xg = (tn % 8 == 0) ? 1 : 0;
         else xg = (tm % 8 == 0) ? 2 : 0;
+        // whole split-K slices per XCD: XRS_SG_XCD_SPLIT=1 (A/B; off by default: the zipper measured
+        // 0.213 vs 0.211 ms with it, profiles/r05/xcd_split_ab_r05aj.txt, where the fp64 Grams' HBM reads fell
+        // 56 -> 41 MB per launch at an unchanged step)
+        const char* e = std::getenv("XRS_SG_XCD_SPLIT");
+        if (e && e[0] == '1' && splits >= 8 && splits % 8 == 0) xg = 3;
     }
     // split-K slabs: one accumulator-layout tile per slice and tile (the in-launch combine reads them)
     DevBuf slab;
