@@ -716,10 +716,13 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
-    // XRS_GLDS_XCD_SPLIT=0 (A/B): the plain slice order
+    // XRS_GLDS_XCD_SPLIT=1: whole (entry, slice) pairs per XCD (opt-in: the step's Grams read 56 -> 41 MB
+    // of HBM per launch at an unchanged step time, profiles/r05/xcd_split_ab_r05aj.txt, and the world-2
+    // gloo cfg5 truncation on one GPU lost orthogonality with it twice in two runs, which the plain order
+    // has not -- not understood, so not the default)
     static const bool xcd_split = [] {
         const char* e = std::getenv("XRS_GLDS_XCD_SPLIT");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     if (xcd_split && splits >= 2 && (count * splits) % 8 == 0) xg = 3;   // whole (entry, split-K slice) pairs per XCD
     // executed K-depth summed over the tile rows / columns (triangular operands skip their zero blocks)
