@@ -200,7 +200,7 @@ __device__ __forceinline__ void gemm_finish(d4 (&acc2)[NACC][TM][TN], double* ld
                     const size_t o = size_t(row) * N + col;
                     double sum = 0.0;
                     for (int z = 0; z < int(gridDim.z); ++z)
-                        sum += (z == int(blockIdx.z)) ? acc[i][j][r]
+                        sum += (z == zb) ? acc[i][j][r]
                                                       : __hip_atomic_load(&slab[(size_t(bz) * gridDim.z + z) * MN + o], __ATOMIC_RELAXED,
                                                                           __HIP_MEMORY_SCOPE_AGENT);
                     C[o] = alpha * sum;
@@ -716,13 +716,14 @@ static void launch_glds(xrs_handle_t h, const PTR& P, int count, size_t lda, boo
     int xg = 0;
     if (double(N) >= double(M)) xg = (tiles_n % 8 == 0) ? 1 : 0;
     else xg = (tiles_m % 8 == 0) ? 2 : 0;
-    // XRS_GLDS_XCD_SPLIT=1: whole (entry, slice) pairs per XCD (opt-in: the step's Grams read 56 -> 41 MB
-    // of HBM per launch at an unchanged step time, profiles/r05/xcd_split_ab_r05aj.txt, and the world-2
-    // gloo cfg5 truncation on one GPU lost orthogonality with it twice in two runs, which the plain order
-    // has not -- not understood, so not the default)
+    // whole (entry, slice) pairs per XCD: the step's GEMMs read 27.4 -> 20.3 MB of HBM per launch (the Grams
+    // 56 -> 41 MB, the batched orthogonality Grams 252 -> 63 MB) at an unchanged step time
+    // (profiles/r05/xcd_split_ab_r05aj.txt). XRS_GLDS_XCD_SPLIT=0: the plain order (A/B). (Its first
+    // version summed the in-launch combine with the hardware slice index instead of the remapped one; the
+    // world-2 cfg5 truncation test caught it, profiles/r05/cfg5_sharded_xcd_split_fail_r05.log.)
     static const bool xcd_split = [] {
         const char* e = std::getenv("XRS_GLDS_XCD_SPLIT");
-        return e && e[0] == '1';
+        return !(e && e[0] == '0');
     }();
     if (xcd_split && splits >= 2 && (count * splits) % 8 == 0) xg = 3;   // whole (entry, split-K slice) pairs per XCD
     // executed K-depth summed over the tile rows / columns (triangular operands skip their zero blocks)
