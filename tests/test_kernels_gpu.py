@@ -103,6 +103,9 @@ BATCHED = [
     (3, 256, 256, 5120, True, False),
     (5, 33, 65, 700, True, True),        # ragged tiles
     (40, 64, 64, 64, False, False),      # more entries than one launch holds (32)
+    (4, 64, 128, 256, False, False),     # 2 tiles x 4 entries x 2 split-K slices, small slabs: the in-launch combine
+    (4, 64, 128, 256, True, True),       # under the XCD-grouped (entry, slice) order, a non-identity remap (r05: the
+                                         # combine's own slice is the remapped one, not blockIdx.z)
     (1, 17, 19, 23, False, False),
 ]
 
