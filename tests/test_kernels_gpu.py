@@ -138,6 +138,8 @@ SYMS = [
     (100, 3000, False, True),   # ragged tiles across the diagonal
     (512, 10240, False, True),  # cfg5
     (33, 17, True, False),
+    (48, 6000, True, False),    # 16 x 16 tiled reduce over 32 x 32 GEMM tiles (N not a tile multiple)
+    (160, 8192, False, True),   # tiled reduce, 55 slices (two chunks)
 ]
 
 

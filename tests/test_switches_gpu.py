@@ -53,8 +53,10 @@ def _bars(r):
     ({"XRS_SGEMM": "1,8"}, lambda r, err: True),                                       # forced fp32 tile / split
     ({"XRS_GLDS_XCD_SPLIT": "0"}, lambda r, err: True),                                # plain split-K order
     ({"XRS_SG_XCD_SPLIT": "1"}, lambda r, err: True),                                  # fp32 split-K per XCD
+    ({"XRS_REDUCE_SYM": "0"}, lambda r, err: True),                                    # elementwise sym reduce
 ], ids=["default", "dot_gate", "gemm_glds", "gemm_cfg", "no_general", "trunc_jacobi", "syev_max", "debug_round",
-        "stamps", "sync_debug", "jacobi_no_early", "glds_st2", "sg_target", "sgemm", "glds_xcd_split", "sg_xcd_split"])
+        "stamps", "sync_debug", "jacobi_no_early", "glds_st2", "sg_target", "sgemm", "glds_xcd_split", "sg_xcd_split",
+        "reduce_sym"])
 def test_switch(env, check):
     r, err = _probe(env)
     _bars(r)

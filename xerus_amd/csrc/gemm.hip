@@ -654,6 +654,30 @@ k_gemm_glds(const PTR ptrs, size_t lda, size_t ldb, int M, int N, int K, int kps
     XRS_TRACE_END
 }
 
+#ifndef XRS_REDUCE_CHUNK
+#define XRS_REDUCE_CHUNK 16
+#endif
+constexpr int kReduceChunk = XRS_REDUCE_CHUNK;
+
+// sum over the split-K slabs of element i, in slice order 0..splits-1 (bitwise identical to the in-launch
+// combine); the loads of kReduceChunk slices are issued together ahead of their dependent adds. Chunk
+// 16 / 20 / 24 / 32 / 48 over the bench step's reduces (40-slice Grams, 16-slice 256^2 products; rocprof
+// averages under the step's concurrency): 6.0-6.2 / 6.2-6.3 / 6.0-6.8 / 6.9-7.1 / 8.1 us
+// (profiles/r05/reduce_chunk_ab_r05.txt)
+__device__ __forceinline__ double slice_sum(const double* __restrict__ slab, size_t MN, int splits, size_t i) {
+    double s = 0.0;
+    for (int z0 = 0; z0 < splits; z0 += kReduceChunk) {
+        double v[kReduceChunk];
+#pragma unroll
+        for (int u = 0; u < kReduceChunk; ++u)
+            v[u] = (z0 + u < splits) ? __builtin_nontemporal_load(&slab[size_t(z0 + u) * MN + i]) : 0.0;
+#pragma unroll
+        for (int u = 0; u < kReduceChunk; ++u)
+            if (z0 + u < splits) s += v[u];
+    }
+    return s;
+}
+
 template <class PTR>
 __global__ void __launch_bounds__(256) k_splitk_reduce(const PTR ptrs, const double* __restrict__ slab, size_t MN,
                                                        int splits, double alpha, int symN) {
@@ -667,21 +691,60 @@ __global__ void __launch_bounds__(256) k_splitk_reduce(const PTR ptrs, const dou
             col = i - row * size_t(symN);
             if (col > row) continue;
         }
-        // slabs summed in slice order 0..splits-1 (bitwise identical to the in-launch combine); the loads
-        // of up to 32 slices are issued together ahead of their dependent adds (one round trip per 32
-        // slices: the step's Grams have 16..24; 8 per round trip measured 10-11 us per 256^2 x 23 reduce)
-        double s = 0.0;
-        for (int z0 = 0; z0 < splits; z0 += 32) {
-            double v[32];
-#pragma unroll
-            for (int u = 0; u < 32; ++u) v[u] = (z0 + u < splits) ? __builtin_nontemporal_load(&slab[size_t(z0 + u) * MN + i]) : 0.0;
-#pragma unroll
-            for (int u = 0; u < 32; ++u)
-                if (z0 + u < splits) s += v[u];
-        }
-        C[i] = alpha * s;
-        if (symN) C[col * size_t(symN) + row] = alpha * s;
+        const double s = alpha * slice_sum(slab, MN, splits, i);
+        C[i] = s;
+        if (symN) C[col * size_t(symN) + row] = s;
     }
+}
+
+// Symmetric results by 16 x 16 tiles of the lower triangle (blockIdx.x = ti (ti + 1) / 2 + tj, tj <= ti): every
+// thread sums one element, and the tile's mirror goes out through LDS as whole 128-B row segments (the
+// elementwise form above writes the mirror one column at a time: a line per lane). Same per-element sums.
+constexpr int kSymTile = 16;
+template <class PTR>
+__global__ void __launch_bounds__(256) k_splitk_reduce_sym(const PTR ptrs, const double* __restrict__ slab, int N,
+                                                           int splits, double alpha) {
+    __shared__ double t[kSymTile][kSymTile + 1];
+    double* __restrict__ C = ptrs.c(blockIdx.y);
+    const size_t MN = size_t(N) * N;
+    slab += size_t(blockIdx.y) * splits * MN;
+    int ti = int((sqrt(8.0 * blockIdx.x + 1.0) - 1.0) * 0.5);
+    while ((ti + 1) * (ti + 2) / 2 <= int(blockIdx.x)) ++ti;
+    while (ti * (ti + 1) / 2 > int(blockIdx.x)) --ti;
+    const int tj = int(blockIdx.x) - ti * (ti + 1) / 2;
+    const int r = int(threadIdx.x) / kSymTile, c = int(threadIdx.x) % kSymTile;
+    const size_t row = size_t(ti) * kSymTile + r, col = size_t(tj) * kSymTile + c;
+    const bool diag = ti == tj;
+    // (a diagonal tile's upper elements take their mirror's value: the result is exactly symmetric)
+    const double s = (!diag || c <= r) ? alpha * slice_sum(slab, MN, splits, row * N + col) : 0.0;
+    t[c][r] = s;
+    __syncthreads();
+    C[row * N + col] = (diag && c > r) ? t[r][c] : s;
+    if (!diag) C[(size_t(tj) * kSymTile + r) * N + size_t(ti) * kSymTile + c] = t[r][c];
+}
+
+// the split-K slabs -> C (alpha applied). XRS_REDUCE_SYM=0: symmetric results through the elementwise kernel
+// (A/B of the tiled form).
+template <class PTR>
+static void splitk_reduce(xrs_handle_t h, const PTR& P, int count, const double* slab, int M, int N, int splits,
+                          double alpha, bool sym) {
+    static const bool sym_tiled = [] {
+        const char* e = std::getenv("XRS_REDUCE_SYM");
+        return !(e && e[0] == '0');
+    }();
+    const size_t MN = size_t(M) * N;
+    KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
+    if (sym && sym_tiled && N % kSymTile == 0) {
+        const unsigned T = unsigned(N / kSymTile);
+        hipLaunchKernelGGL(k_splitk_reduce_sym<PTR>, dim3(T * (T + 1) / 2, unsigned(count)), dim3(256), 0, h->stream, P, slab,
+                           N, splits, alpha);
+        check_launch("k_splitk_reduce_sym");
+        return;
+    }
+    const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
+    hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab, MN, splits,
+                       alpha, sym ? N : 0);
+    check_launch("k_splitk_reduce");
 }
 
 template <int BM, int BN, int GBK, int WGM, int WGN, int WGK, int PD, class PTR>
@@ -853,14 +916,7 @@ static bool gemm_glds(xrs_handle_t h, const PTR& P, int count, int M, int N, int
         default: XRS_GLDS(32, 32, 2, 2, 1); break;
     }
 #undef XRS_GLDS
-    if (splits > 1 && tickets == nullptr) {
-        const size_t MN = size_t(M) * N;
-        const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
-        KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
-        hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab.d(), MN,
-                           splits, alpha, sym ? N : 0);
-        check_launch("k_splitk_reduce");
-    }
+    if (splits > 1 && tickets == nullptr) splitk_reduce(h, P, count, slab.d(), M, N, splits, alpha, sym);
     return true;
 }
 
@@ -972,14 +1028,7 @@ static void gemm_impl(xrs_handle_t h, const PTR& P, int count, size_t Ms, size_t
         default: XRS_TILES(32, 32, 16, 2, 2, 2, 2); break;
     }
 #undef XRS_TILES
-    if (splits > 1 && tickets == nullptr) {
-        const size_t MN = size_t(M) * N;
-        const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
-        KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
-        hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab.d(), MN,
-                           splits, alpha, sym ? N : 0);
-        check_launch("k_splitk_reduce");
-    }
+    if (splits > 1 && tickets == nullptr) splitk_reduce(h, P, count, slab.d(), M, N, splits, alpha, sym);
 }
 
 void gemm(xrs_handle_t h, double* C, size_t Ms, size_t Ns, double alpha, const double* A, size_t lda, bool ta, size_t Ks,
