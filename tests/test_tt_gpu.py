@@ -47,6 +47,12 @@ def test_dot(handle, ref, dims, ranks):
     nx, ny = np.sqrt(ref.dot(x, x)), np.sqrt(ref.dot(y, y))
     assert abs(d_gpu - d_ref) <= 1e-12 * nx * ny
     assert abs(gx.dot(gx) - nx * nx) <= 1e-12 * nx * nx
+    # <x, x> on the same cores takes the symmetric environments (gemm_sym); a copy of x (other pointers)
+    # takes the general products: both the same value to rounding, the async form bitwise the sync one
+    gx2 = capi.TTDevice.from_cores(handle, x.cores)
+    assert abs(gx.dot(gx) - gx.dot(gx2)) <= 1e-13 * nx * nx
+    if len(dims) >= 4:
+        assert gx.dot_async(gx).result() == gx.dot(gx)
     # the asynchronous form runs the same two-ended zipper on the side streams: bitwise the same value
     # from order 4 on (below, the synchronous form is one-ended)
     d_async = gx.dot_async(gy).result()
