@@ -129,6 +129,27 @@ def bench_cfg5(h, xe, world, rank, dist, sync, steps, warmup):
         elapsed = float(t.item())
     f = flops_round(dims, ranks)
     ms = elapsed / steps * 1e3
+    # the truncating round(256) of the same TT (rank 512 -> 256; BASELINE.md §2 quotes the reference at 31.9 s /
+    # 13.3 s for it): a fresh copy of the slices per call, host-timed, max over ranks
+    trunc_ms, paths = [], set()
+    for i in range(3):
+        c = xd.ShardedTT(h, st.local.clone(), st.dims, world, rank)
+        sync()
+        t1 = time.perf_counter()
+        paths.add(c.round_sharded(r // 2, comm) or "uncertified")
+        h.synchronize()
+        sync()
+        t1 = time.perf_counter() - t1
+        if dist is not None:
+            import torch
+
+            t = torch.tensor([t1], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            t1 = float(t.item())
+        if i:
+            trunc_ms.append(t1 * 1e3)
+        trunc_ranks = c.ranks
+        c.local.free()
     out = {
         "workload": f"TT order-{d} n={n} rank-{r}: round({r}) sharded by mode slices over {world} rank(s)",
         "ms_per_round": round(ms, 3),
@@ -140,6 +161,12 @@ def bench_cfg5(h, xe, world, rank, dist, sync, steps, warmup):
         "allreduce_per_round": (comm.calls - calls0) / steps,
         "allreduce": comm_kind,
         "steps": steps,
+        "round256_truncating": {
+            "ms": round(float(np.mean(trunc_ms)), 3), "calls": len(trunc_ms), "path": sorted(paths),
+            "ranks_out": trunc_ranks,
+            "note": "x.round(256) from rank 512 (xrs_tt_round_sharded_ex on each rank's slices), host wall per call "
+                    "after one untimed call, max over ranks",
+        },
     }
     if hasattr(comm, "close"):
         comm.close()
@@ -394,9 +421,63 @@ def host_cpu_info():
     return {"nproc": nproc, "affinity": affinity, "model": model, "threads": max(1, threads), "rule": rule}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, worker=None, timeout=None):
+    """`bench.py --gpus N` without a launcher around it: start N rank processes, one per GPU, and relay rank 0's
+    JSON line. Runs BEFORE anything touches the GPU -- this process imports neither torch nor xerus_amd and
+    never execs: the ranks are ordinary child processes (python bench.py ... with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment, the torch.distributed.run
+    contract), so each binds its own device and joins the nccl (RCCL) process group itself. Returns the
+    exit status: 0 only if every rank exited 0. `worker` replaces this script (tests: a stub rank)."""
+    import subprocess
+    import tempfile
+
+    worker = worker or os.path.abspath(__file__)
+    port = _free_port()
+    procs = []
+    with tempfile.TemporaryFile(mode="w+") as out0:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+            env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (RCCL across processes on this image)
+            procs.append(subprocess.Popen([sys.executable, worker] + list(argv), env=env,
+                                          stdout=out0 if r == 0 else subprocess.DEVNULL))
+        # wait for all; a failed rank ends the job (the others would wait for it in a collective forever)
+        t0 = time.time()
+        bad = []
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad or all(c == 0 for c in codes):
+                break
+            if timeout is not None and time.time() - t0 > timeout:
+                bad = [(r, "timeout") for r, c in enumerate(codes) if c is None]
+                break
+            time.sleep(0.05)
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        if bad:
+            print(f"[bench] rank(s) failed: {bad}", file=sys.stderr)
+        out0.seek(0)
+        lines = [ln for ln in out0.read().splitlines() if ln.strip()]
+    if lines:
+        print(lines[-1], flush=True)
+    return 0 if not bad and lines else 1
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node; N > 1 without WORLD_SIZE in the environment starts N rank processes")
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--order", type=int, default=10)
@@ -411,7 +492,12 @@ def main():
                     help="skip the per-config lines (cfg1-cfg4, permutation roofline, SVD); they run at N=1 only")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us (python bench.py --gpus N): become it, before any GPU or torch import
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: measuring {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -596,7 +682,7 @@ def main():
             },
         }
         cpu = None
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:   # the CPU baseline is an N = 1 figure (rank 0 of a single-GPU run)
             # CPU baseline leg: the oracle (numpy/scipy-LAPACK restatement of the reference algorithm)
             from oracle import xerus_ref as ref
 

@@ -265,7 +265,10 @@ int xrs_comm_allreduce(void* comm, double* buf, size_t count);
  *  IDENTICAL mode slices, i.e. the sharding of the TT whose every mode is the local one repeated nranks
  *  times. xrs_comm_allreduce on it enqueues buf *= nranks (exactly that TT's sum over ranks) on the handle's
  *  stream; all-gather is refused. A diagnostic: the sharded round then runs a real rank's kernels, with
- *  collectives of zero cost (tools/cfg5_rank_probe.py). */
+ *  collectives of zero cost (tools/cfg5_rank_probe.py). Limitation: a core gathered through
+ *  it (a zero-padded block all-reduced) would be nranks x rank 0's block, not the TT's core, so the steps
+ *  that gather -- tall right edges, left structural-excess QC -- treat the layout as unknown and the round
+ *  reports uncertified (path 0) instead. */
 int xrs_comm_emulate(xrs_handle_t handle, int nranks, xrs_comm_t* comm_out);
 /** xrs_allgather_fn of the communicator: ncclAllGather (fp64) enqueued on the handle's stream. */
 int xrs_comm_allgather(void* comm, const double* send, double* recv, size_t count);

@@ -168,3 +168,28 @@ def test_emulated_comm_rank0_of_replicated_tt(handle, ref):
         assert comm.calls > 0
     finally:
         comm.close()
+
+
+def test_emulated_comm_tall_right_edge_reports_uncertified(handle, ref):
+    """under xrs_comm_emulate a core "gathered" by the all-reduce of a zero-padded block is nranks x
+    rank 0's block, not the TT's core. A sum whose right edge is tall (r_{d-1} = 4 > n = 3) and whose first edge
+    has structural excess needs such gathers: the round must report uncertified (path "") and leave the
+    represented tensor as it was, not factorise a wrong matrix."""
+    from xerus_amd import capi
+    from xerus_amd import dist as xd
+
+    d, world = 5, 3
+    x = ref.TT.random_raw([1] * d, [2] * (d - 1), ref.Rng(51))
+    y = ref.TT.random_raw([1] * d, [2] * (d - 1), ref.Rng(52))
+    s = ref.tt_add(x, y)   # local mode size 1 (global 3), ranks 4: tall right edge, left excess
+    before = ref.TT([c.copy() for c in s.cores]).full()
+    comm = xd.EmulatedComm(handle, world)
+    try:
+        st = xd.ShardedTT(handle, capi.TTDevice.from_cores(handle, s.cores), [world] * d, world, 0)
+        path = st.round_sharded(3, comm)
+        assert path == "", path
+        after = ref.TT(st.local.cores()).full()
+        assert np.linalg.norm(after - before) <= 1e-12 * np.linalg.norm(before)
+        st.local.free()
+    finally:
+        comm.close()

@@ -66,6 +66,11 @@ void check_nccl(ncclResult_t r, const char* what) {
 }
 
 }  // namespace
+
+// an xrs_comm_emulate communicator (the per-rank timing probe): its all-reduce is nranks x the local value,
+// so a zero-padded core "gathered" through it is not the TT's core (tt_trunc.hip: shard_layout)
+bool comm_is_emulated(const void* ctx) { return ctx && static_cast<const xrs_comm_s*>(ctx)->emulated; }
+
 }  // namespace xrs
 
 using namespace xrs;

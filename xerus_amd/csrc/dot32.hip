@@ -227,12 +227,17 @@ double dot_f32(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
         const int e = int((bits >> 23) & 0xff) - 127;   // floor(log2 max)
         if (bits != 0u && (bits >= 0x7f800000u || e < -100 || e >= 100)) return tt::dot(h, d, n, rx, X, ry, Y);
     }
+    // a product that left the fp32 range anyway (a max word or the closing sum not finite: products bounded
+    // by (n r)^2 max|core|^2 can still overflow at rank products near the 2^30 limit): the fp64 zipper
+    for (size_t i = 0; i < 4 * d + 2; ++i)
+        if (hw[i] >= 0x7f800000u) return tt::dot(h, d, n, rx, X, ry, Y);
     double v = 0.0;
     for (int blk = 0; blk < kPairBlocks; ++blk) {
         double p;
         std::memcpy(&p, hs + 8 * blk, 8);
         v += p;
     }
+    if (!std::isfinite(v)) return tt::dot(h, d, n, rx, X, ry, Y);
     // the powers of two the products scaled their normalised operands by: left E_k (k = 1..m-1; E_0 = [1]:
     // 2^-1) and T of cores 0..m-1, right F_k (k = m+1..d-1; F_d = [1]: 2^-1) and T of cores m..d-1
     int e = 2 * pow2_exponent(0x3f800000u);

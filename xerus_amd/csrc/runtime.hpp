@@ -225,4 +225,7 @@ class StreamFork {
     bool joined_ = false;
 };
 
+// an xrs_comm_emulate communicator (comm.cpp): its all-reduce is nranks x the local value
+bool comm_is_emulated(const void* ctx);
+
 }  // namespace xrs

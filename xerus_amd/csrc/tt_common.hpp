@@ -41,6 +41,11 @@ struct TT {
     // (tall right edges, structural-excess QC steps) cannot be gathered and the round reports uncertified
     int world = 0;
     int rank = 0;
+    // shard_layout's result, computed once per TT (its all-reduce and host wait are paid once per round even
+    // when the certified truncation falls through to the general round)
+    bool layout_cached = false;
+    std::vector<size_t> layout_ng, layout_off;
+    bool layout_known = false;
     bool sharded() const { return shard_mode; }
     void reduce(double* buf, size_t count) const {
         if (!ar) return;

@@ -237,6 +237,12 @@ void left_pass(Sweep& sw, TT& t0, double* const* src, bool certify, std::vector<
 ShardLayout shard_layout(TT& t) {
     const size_t d = t.d;
     ShardLayout lay;
+    if (t.layout_cached) {
+        lay.ng = t.layout_ng;
+        lay.off = t.layout_off;
+        lay.known = t.layout_known;
+        return lay;
+    }
     lay.ng.assign(t.n, t.n + d);
     lay.off.assign(d, 0);
     lay.known = !t.sharded();
@@ -264,7 +270,14 @@ ShardLayout shard_layout(TT& t) {
         lay.ng[k] = s;
         lay.off[k] = o;
     }
-    lay.known = t.world > 0;
+    // an emulated communicator (rank 0 of identical slices) sums a zero-padded core to nranks x rank 0's
+    // block, not the TT's core: the layout counts as unknown, so the steps that need a gathered core (tall
+    // right edges, left structural excess) report uncertified instead of factorising a wrong matrix
+    lay.known = t.world > 0 && !(t.ar == &xrs_comm_allreduce && comm_is_emulated(t.ar_ctx));
+    t.layout_cached = true;
+    t.layout_ng = lay.ng;
+    t.layout_off = lay.off;
+    t.layout_known = lay.known;
     return lay;
 }
 

@@ -177,7 +177,9 @@ class RcclComm:
 
 class EmulatedComm(RcclComm):
     """xrs_comm_emulate: rank 0 of `world` ranks holding identical slices (the sum over ranks is `world` x the
-    local value, enqueued on the stream). Per-rank timing of the sharded path on one GPU; not a collective."""
+    local value, enqueued on the stream). Per-rank timing of the sharded path on one GPU; not a collective.
+    Rounds whose steps need a gathered core (tall right edges, left structural excess) report uncertified under
+    it: a zero-padded core summed this way is not the TT's core."""
 
     def __init__(self, handle: capi.Handle, world: int):
         self.handle, self.lib = handle, handle.lib
