@@ -76,6 +76,26 @@ def main():
     e_ref, _ = tt_diff_norm(og.cores, xg.cores)
     out["graded_ranks_ok"] = gg.ranks == og.ranks
     out["graded_err_diff"] = abs(e_gpu - e_ref) / nrm
+    # flat spectra cut inside the cluster (the Jacobi early stop on repeated singular values): x has
+    # cores that are left- AND right-orthonormal, so every edge's singular values are all 1; x + x is rank
+    # deficient (general path) with edge spectra {2 (r times), 0}; round(r / 2) cuts inside the cluster. The kept
+    # subspace is not unique there, the ranks and the truncation error are
+    fr, fn, fd = 10, 10, 6
+    frng = np.random.default_rng(11)
+    fc = [np.linalg.qr(frng.standard_normal((fn, fr)))[0].reshape(1, fn, fr)]
+    for _ in range(fd - 2):
+        fc.append(np.stack([np.linalg.qr(frng.standard_normal((fr, fr)))[0] for _ in range(fn)], axis=1) / np.sqrt(fn))
+    fc.append(np.linalg.qr(frng.standard_normal((fn, fr)))[0].T.reshape(fr, fn, 1))
+    xs = ref.tt_add(ref.TT(fc), ref.TT([c.copy() for c in fc]))
+    gf = capi.TTDevice.from_cores(h, [c.copy() for c in xs.cores])
+    gf.round(fr // 2)
+    out["flat_path"] = h.last_round_path()
+    of = xs.copy()
+    of.round(fr // 2)
+    e_gpu, nrm = tt_diff_norm(gf.cores(), xs.cores)
+    e_ref, _ = tt_diff_norm(of.cores, xs.cores)
+    out["flat_ranks_ok"] = gf.ranks == of.ranks
+    out["flat_err_diff"] = abs(e_gpu - e_ref) / nrm
     # the block Jacobi right singular vectors (xrs_svd_rows_vt) and the eigensolver entry (xrs_sym_eig_top)
     W = rng.standard_normal((64, 96))
     S, Vt, sweeps = h.svd_rows_vt(h.array(W))

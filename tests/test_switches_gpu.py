@@ -33,11 +33,12 @@ def _bars(r):
     assert r["chain_path"] == "chain" and r["chain_err"] <= 1e-10
     assert r["trunc_ranks_ok"] and r["trunc_err_diff"] <= 1e-6
     assert r["graded_ranks_ok"] and r["graded_err_diff"] <= 1e-6
+    assert r["flat_ranks_ok"] and r["flat_err_diff"] <= 1e-6
     assert r["svd_err"] <= 1e-12 and r["eig_err"] <= 1e-12
 
 
 @pytest.mark.parametrize("env,check", [
-    ({}, lambda r, err: r["trunc_path"] == "truncate" and r["graded_path"] == "general"),
+    ({}, lambda r, err: r["trunc_path"] == "truncate" and r["graded_path"] == "general" and r["flat_path"] == "general"),
     ({"XRS_DOT_GATE": "0"}, lambda r, err: True),                                      # ungated async product
     ({"XRS_GEMM_GLDS": "0"}, lambda r, err: True),                                     # general GEMM kernel only
     ({"XRS_GEMM_CFG": "2,256,512"}, lambda r, err: True),                              # forced 64x64 tiles
@@ -47,7 +48,7 @@ def _bars(r):
     ({"XRS_DEBUG_ROUND": "1"}, lambda r, err: "round_truncate:" in err and "round_general:" in err),
     ({"XRS_STAMPS": "all"}, lambda r, err: "[round host us]" in err and "jacobi_vt p=" in err and "k_sytrd n=" in err),
     ({"XRS_SYNC_DEBUG": "1"}, lambda r, err: "[xrs] launched k_gemm" in err),
-    ({"XRS_JACOBI_NO_EARLY": "1"}, lambda r, err: r["graded_path"] == "general"),     # confirming Jacobi sweep
+    ({"XRS_JACOBI_NO_EARLY": "1"}, lambda r, err: r["graded_path"] == "general" and r["flat_path"] == "general"),
     ({"XRS_GLDS_ST2": "0"}, lambda r, err: True),                                      # 3-stage LDS-DMA tiles
     ({"XRS_SG_TARGET": "96"}, lambda r, err: True),                                    # fp32 split-K target
     ({"XRS_SGEMM": "1,8"}, lambda r, err: True),                                       # forced fp32 tile / split

@@ -195,8 +195,27 @@ void SinglePointMeasurementSet::measure(const TTTensor& _solution) {
     measuredValues = internal::evaluate_tt(_solution, dm);
 }
 
+namespace {
+// A network whose full tensor is small next to the work of contracting it once per entry (TensorNetwork::
+// operator[], a slice copy per external mode and a contraction per entry) is contracted once and every entry
+// read from the full tensor: at most 2^22 entries, or 64 per measurement.
+bool contract_whole(const TensorNetwork& _net, size_t _count) {
+    const size_t limit = std::max<size_t>(size_t(1) << 22, 64 * _count);
+    size_t s = 1;
+    for (const size_t d : _net.dimensions) {
+        if (d != 0 && s > limit / d) return false;
+        s *= d;
+    }
+    return true;
+}
+}  // namespace
+
 void SinglePointMeasurementSet::measure(const TensorNetwork& _solution) {
     XERUS_REQUIRE(_solution.degree() == degree(), "Degrees of solution and measurements must match!");
+    if (contract_whole(_solution, size())) {
+        measure(_solution.to_tensor());
+        return;
+    }
     for (size_t i = 0; i < size(); ++i) measuredValues[i] = _solution[positions[i]];
 }
 
@@ -216,6 +235,7 @@ double SinglePointMeasurementSet::test(const Tensor& _solution) const {
 
 double SinglePointMeasurementSet::test(const TensorNetwork& _solution) const {
     XERUS_REQUIRE(_solution.degree() == degree(), "Degrees of solution and measurements must match!");
+    if (contract_whole(_solution, size())) return test(_solution.to_tensor());
     double error = 0.0, norm = 0.0;
     for (size_t i = 0; i < size(); ++i) {
         const double e = measuredValues[i] - _solution[positions[i]];

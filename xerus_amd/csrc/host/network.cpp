@@ -530,7 +530,11 @@ value_t TensorNetwork::operator[](const std::vector<size_t>& _positions) const {
     for (size_t i = 0; i < degree(); ++i)
         XERUS_REQUIRE(_positions[i] < dimensions[i], "Position " << _positions[i] << " out of range in mode " << i);
     // the reference's partial copy (tensorNetwork.cpp:331-370): fix every node's external modes (slices of the
-    // device tensors), drop the external links, renumber the internal ones, contract what remains
+    // device tensors), drop the external links, renumber the internal ones, contract what remains.
+    // Cost per entry: the node copies are copy-on-write handles (no device copy); each external mode is one
+    // strided slice copy, then the network of slices is contracted (one launch chain per entry). Callers that
+    // need many entries of a TT -- the measurement sets of ADF -- go through the batched M x r stacks of
+    // adf.hip instead (host/adf.cpp), not through this operator.
     TensorNetwork partial{Structure{}};
     partial.nodes = nodes;
     for (TensorNode& node : partial.nodes) {
