@@ -26,6 +26,13 @@ pytestmark = pytest.mark.gpu
     ([20] * 12, [256] * 11, 1.0),                    # cfg4 shape
     ([20] * 10, [64] * 9, 1e6),                      # ||x|| ~ 1e66: beyond fp32 without the renormalisation
     ([20] * 10, [64] * 9, 1e-6),                     # ||x|| ~ 1e-54
+    # the fused zipper (zip32.hip): heads only (d = 4), one end without a step (d = 5), uneven step counts
+    # (d = 7), the headline shape at other scales (per-unit T exponents, exponent words)
+    ([20] * 4, [20, 128, 20], 1.0),
+    ([8] * 5, [8, 64, 64, 8], 1.0),
+    ([10] * 7, [10, 96, 96, 96, 96, 10], 1.0),
+    ([20] * 10, [20] + [256] * 7 + [20], 1e5),
+    ([20] * 10, [20] + [256] * 7 + [20], 1e-5),
 ])
 def test_dot_f32(handle, ref, dims, ranks, scale):
     rng = ref.Rng(11)
@@ -77,13 +84,16 @@ def test_dot_f32_correlated(handle, ref, dims, ranks):
     assert abs(d32 - d_ref) <= 1e-6 * abs(d_ref), (d32, d_ref, abs(d32 - d_ref) / abs(d_ref))
 
 
-@pytest.mark.parametrize("scale,d", [(1e-40, 3), (1e40, 3), (1e-25, 4), (1e25, 4), (1e9, 4), (1e-15, 4)])
+@pytest.mark.parametrize("scale,d", [(1e-40, 3), (1e40, 3), (1e-25, 4), (1e25, 4), (1e9, 4), (1e-15, 4),
+                                     (1e-12, 6), (1e12, 6), (1e9, 6), (1e-15, 6)])
 def test_dot_f32_core_range(handle, ref, scale, d):
-    """Both TTs' cores scaled: 1e+-40 lies outside the fp32 zipper's core range [2^-100, 2^100) and
+    """Both TTs' cores scaled (d = 6 through the fused zipper's fp32 steps, where 1e+-40 would leave
+    the fp64 range of the reference value itself): 1e+-40 lies outside the fp32 zipper's core range [2^-100, 2^100) and
     must come back as the fp64 result (the fp64 zipper takes over); 1e+-25, 1e9, 1e-15 lie inside and run in
     fp32 at fp32 accuracy (every product has one raw core and one power-of-two normalised operand)."""
     rng = ref.Rng(31)
-    dims, ranks = [20] * d, [20] * (d - 1)
+    # d = 6: ranks 20 / 64 (x + z: 40 / 128), the fused zipper's heads and fp32 steps (zip32.hip)
+    dims, ranks = [20] * d, ([20] * (d - 1) if d < 6 else [20] + [64] * (d - 3) + [20])
     x = ref.TT.random_raw(dims, ranks, rng)
     z = ref.TT.random_raw(dims, ranks, rng)
     y = ref.tt_add(x, z)
@@ -97,3 +107,56 @@ def test_dot_f32_core_range(handle, ref, scale, d):
     assert np.isfinite(d32) and d32 != 0.0
     tol = 1e-12 if scale in (1e-40, 1e40) else 1e-6
     assert abs(d32 - d_ref) <= tol * abs(d_ref), (d32, d_ref, abs(d32 - d_ref) / abs(d_ref))
+
+
+def test_dot_f32_fused_matches_per_product_form(ref):
+    """XRS_ZIP32=0 (dot32.hip's per-product zipper for every shape) against the default fused zipper at the
+    headline shape and a d = 7 shape, each in its own process (the switch is read once): both within the fp32
+    bar of the fp64 value, and the fused path bitwise repeatable."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    code = r"""
+import json, sys
+sys.path.insert(0, %r)
+import numpy as np
+from oracle import xerus_ref as ref
+from xerus_amd import capi
+h = capi.Handle(0)
+out = []
+for dims, ranks in (([20] * 10, [20] + [256] * 7 + [20]), ([10] * 7, [10, 96, 96, 96, 96, 10])):
+    rng = ref.Rng(77)
+    x = ref.TT.random_raw(dims, ranks, rng)
+    y = ref.TT.random_raw(dims, ranks, rng)
+    gx, gy = capi.TTDevice.from_cores(h, x.cores), capi.TTDevice.from_cores(h, y.cores)
+    a, b = gx.dot_f32(gy), gx.dot_f32(gy)
+    out.append([a, b, ref.dot(x, y), float(np.sqrt(ref.dot(x, x) * ref.dot(y, y)))])
+print(json.dumps(out))
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, XRS_ZIP32=flag)
+        p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-3000:]
+        res[flag] = json.loads(p.stdout.strip().splitlines()[-1])
+    for flag in ("1", "0"):
+        for a, b, d_ref, nn in res[flag]:
+            assert a == b
+            assert abs(a - d_ref) <= 1e-6 * nn, (flag, a, d_ref, nn)
+
+
+def test_dot_f32_fused_core_out_of_range(handle, ref):
+    """One core of x scaled by 2^110 and another by 2^-110 (the TT unchanged up to rounding): the fused zipper
+    (d = 6, fp32 steps) sees a core outside [2^-100, 2^100) and returns the fp64 zipper's value."""
+    rng = ref.Rng(37)
+    dims, ranks = [20] * 6, [20, 64, 64, 64, 20]
+    x = ref.TT.random_raw(dims, ranks, rng)
+    y = ref.TT.random_raw(dims, ranks, rng)
+    x.cores[2] = x.cores[2] * 2.0 ** 110
+    x.cores[3] = x.cores[3] * 2.0 ** -110
+    gx = capi.TTDevice.from_cores(handle, x.cores)
+    gy = capi.TTDevice.from_cores(handle, y.cores)
+    d64, d32 = gx.dot(gy), gx.dot_f32(gy)
+    assert d32 == d64

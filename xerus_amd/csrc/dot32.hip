@@ -19,6 +19,7 @@
 // and to ||x|| ||y|| in general (tests).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "runtime.hpp"
@@ -205,6 +206,13 @@ double dot_f32(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
                const double* const* Y) {
     XRS_REQUIRE(d >= 2 && d <= 2048, "the fp32 zipper takes 2..2048 components");
     for (size_t k = 0; k <= d; ++k) XRS_REQUIRE(rx[k] * ry[k] < (size_t(1) << 30), "fp32 zipper: rank product too large");
+    // the fused form (zip32.hip: one launch per step for both ends) where the shapes allow it; XRS_ZIP32=0 keeps
+    // this per-product form for every shape (A/B runs)
+    static const bool no_zip = [] {
+        const char* e = std::getenv("XRS_ZIP32");
+        return e && e[0] == '0';
+    }();
+    if (!no_zip && zip::applicable(d, n, rx, X, ry, Y)) return zip::dot(h, d, n, rx, X, ry, Y);
     const size_t m = d / 2;
     size_t off[7];
     Dot32Bufs b{};

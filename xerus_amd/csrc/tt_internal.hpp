@@ -14,4 +14,10 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
 void soft_threshold(xrs_handle_t h, size_t d, const size_t* n, size_t* r, double** cores, bool canonicalized, size_t core_pos,
                     const double* taus);
 }  // namespace tt
+namespace zip {   // zip32.hip: the fused fp32 zipper (xrs_tt_dot_f32's main path)
+bool applicable(size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+                const double* const* Y);
+double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y);
+}  // namespace zip
 }  // namespace xrs
