@@ -110,9 +110,11 @@ def test_dot_f32_core_range(handle, ref, scale, d):
 
 
 def test_dot_f32_fused_matches_per_product_form(ref):
-    """XRS_ZIP32=0 (dot32.hip's per-product zipper for every shape) against the default fused zipper at the
-    headline shape and a d = 7 shape, each in its own process (the switch is read once): both within the fp32
-    bar of the fp64 value, and the fused path bitwise repeatable."""
+    """The three forms of the fp32 zipper, each in its own process (the switch is read once): the default
+    (dot32.hip's per-product launches), XRS_ZIP32=1 (zip32.hip's fused front end, then per-product steps) and
+    XRS_ZIP32=2 (fused steps throughout). Cases: the headline shape, heads only (d = 4), one end without a step
+    (d = 5), uneven step counts (d = 7), correlated pairs scaled by 1e+-12 (d = 6: fp32 steps, exponent words) and
+    cores outside [2^-100, 2^100) (fp64 fallback, exact). All within the fp32 bar, bitwise repeatable."""
     import json
     import os
     import subprocess
@@ -126,25 +128,40 @@ from oracle import xerus_ref as ref
 from xerus_amd import capi
 h = capi.Handle(0)
 out = []
-for dims, ranks in (([20] * 10, [20] + [256] * 7 + [20]), ([10] * 7, [10, 96, 96, 96, 96, 10])):
+cases = [([20] * 10, [20] + [256] * 7 + [20], 1.0, 0), ([10] * 7, [10, 96, 96, 96, 96, 10], 1.0, 0),
+         ([20] * 4, [20, 128, 20], 1.0, 0), ([8] * 5, [8, 64, 64, 8], 1.0, 0),
+         ([20] * 6, [20, 64, 64, 64, 20], 1e12, 1), ([20] * 6, [20, 64, 64, 64, 20], 1e-12, 1),
+         ([20] * 6, [20, 64, 64, 64, 20], 1.0, 2)]
+for dims, ranks, scale, kind in cases:
     rng = ref.Rng(77)
     x = ref.TT.random_raw(dims, ranks, rng)
     y = ref.TT.random_raw(dims, ranks, rng)
+    if kind == 1:                      # correlated pair, every core scaled
+        y = ref.tt_add(x, y)
+        x.cores = [c * scale for c in x.cores]
+        y.cores = [c * scale for c in y.cores]
+    if kind == 2:                      # one core above, one below the fp32 zipper's range
+        x.cores[2] = x.cores[2] * 2.0 ** 110
+        x.cores[3] = x.cores[3] * 2.0 ** -110
     gx, gy = capi.TTDevice.from_cores(h, x.cores), capi.TTDevice.from_cores(h, y.cores)
     a, b = gx.dot_f32(gy), gx.dot_f32(gy)
-    out.append([a, b, ref.dot(x, y), float(np.sqrt(ref.dot(x, x) * ref.dot(y, y)))])
+    d_ref = ref.dot(x, y)
+    nn = float(np.sqrt(ref.dot(x, x) * ref.dot(y, y)))
+    out.append([a, b, d_ref, nn, kind, gx.dot(gy)])
 print(json.dumps(out))
 """ % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    res = {}
-    for flag in ("1", "0"):
+    for flag in ("0", "1", "2"):
         env = dict(os.environ, XRS_ZIP32=flag)
         p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
         assert p.returncode == 0, p.stderr[-3000:]
-        res[flag] = json.loads(p.stdout.strip().splitlines()[-1])
-    for flag in ("1", "0"):
-        for a, b, d_ref, nn in res[flag]:
-            assert a == b
-            assert abs(a - d_ref) <= 1e-6 * nn, (flag, a, d_ref, nn)
+        for a, b, d_ref, nn, kind, d64 in json.loads(p.stdout.strip().splitlines()[-1]):
+            assert a == b, (flag, kind)
+            if kind == 2:
+                assert a == d64, (flag, a, d64)
+            elif kind == 1:
+                assert abs(a - d_ref) <= 1e-6 * abs(d_ref), (flag, a, d_ref)
+            else:
+                assert abs(a - d_ref) <= 1e-6 * nn, (flag, a, d_ref, nn)
 
 
 def test_dot_f32_fused_core_out_of_range(handle, ref):

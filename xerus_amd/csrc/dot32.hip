@@ -121,10 +121,30 @@ size_t dot32_layout(size_t d, const size_t* n, const size_t* rx, const size_t* r
     return o;
 }
 
-// enqueues the zipper on h->stream (+ its side stream 0) up to the closing partial sums in b.W
+// Start of the per-product steps: left cores from kl (environment El at edge kl, row stride lde, its max word is
+// L(kl)), right cores from kr down (Fr at edge kr + 1, stride ldf, max word R(kr + 1)); kl = 0 / kr = d - 1 with
+// null environments start from E_0 = F_d = [1].
+struct Dot32Start {
+    size_t kl = 0, kr = size_t(-1);
+    const float* El = nullptr;
+    const float* Fr = nullptr;
+    size_t lde = 0, ldf = 0;
+};
+
+// the zeroing of the words and slots (before anything writes them: a front end's kernels atomicMax into them)
+void dot32_init(xrs_handle_t h, const Dot32Bufs& bf) {
+    const size_t zoff = bf.zero_off - bf.one_off;
+    XRS_REQUIRE(zoff % 4 == 0 && bf.zero_bytes % 4 == 0, "fp32 zipper: misaligned scratch");
+    const unsigned blocks = unsigned(std::min<size_t>((bf.zero_bytes / 4 + 255) / 256, 256));
+    hipLaunchKernelGGL(k_dot32_init, dim3(std::max(1u, blocks)), dim3(256), 0, h->stream, bf.W + bf.one_off, zoff, bf.zero_bytes);
+    check_launch("k_dot32_init");
+}
+
+// enqueues the zipper on h->stream (+ its side stream 0) up to the closing partial sums in b.W (dot32_init first)
 void dot32_enqueue(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
-                   const double* const* Y, const Dot32Bufs& bf) {
+                   const double* const* Y, const Dot32Bufs& bf, const Dot32Start& st = Dot32Start{}) {
     const size_t m = d / 2;
+    const size_t kl = st.kl, kr = st.kr == size_t(-1) ? d - 1 : st.kr;
     float *E = bf.E0, *En = bf.E1, *F = bf.F0, *Fn = bf.F1;
     double* res = reinterpret_cast<double*>(bf.W);
     unsigned* cmax = reinterpret_cast<unsigned*>(bf.W + 8 * kPairBlocks);
@@ -141,30 +161,26 @@ void dot32_enqueue(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, 
     auto sx = [&](size_t k) { return slots + k * kCmaxSlots; };
     auto sy = [&](size_t k) { return slots + (d + k) * kCmaxSlots; };
     {
-        const size_t zoff = bf.zero_off - bf.one_off;
-        XRS_REQUIRE(zoff % 4 == 0 && bf.zero_bytes % 4 == 0, "fp32 zipper: misaligned scratch");
-        const unsigned blocks = unsigned(std::min<size_t>((bf.zero_bytes / 4 + 255) / 256, 256));
-        hipLaunchKernelGGL(k_dot32_init, dim3(std::max(1u, blocks)), dim3(256), 0, h->stream, bf.W + bf.one_off, zoff, bf.zero_bytes);
-        check_launch("k_dot32_init");
-    }
-    {
         StreamFork fork(h);
         // left end (cores 0..m-1) on the side stream, right end (cores d-1..m) on the main stream; launches
         // interleaved step by step so that both streams have work from the start (the host's enqueue rate,
         // not the GPU, paces a chain of small launches). Every product has one raw core and one operand
         // normalised by its max word; E_0 = F_d = [1].
-        for (size_t s = 0; s < std::max(m, d - m); ++s) {
-            if (s < m) {
+        const size_t nl = m - kl, nr = kr + 1 - m;   // steps per end
+        for (size_t s = 0; s < std::max(nl, nr); ++s) {
+            if (s < nl) {
                 fork.side();
-                const size_t k = s;
+                const size_t k = kl + s;
                 const size_t a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
-                const float* Ek = k == 0 ? one : E;
+                const bool first = s == 0;
+                const float* Ek = first ? (st.El ? st.El : one) : E;
+                const size_t lda = first && st.El ? st.lde : b;
                 // T (b x nk a2) = 2^-e E^T X_k
                 SgemmExtra xt;
-                xt.sa = k == 0 ? one_max : L(k);
+                xt.sa = (first && !st.El) ? one_max : L(k);
                 xt.amax = TLw(k);
                 xt.cmax_b = sx(k);
-                sgemm<float, double>(h, bf.TL, b, nk * a2, 1.0f, Ek, b, true, a, X[k], nk * a2, false, xt);
+                sgemm<float, double>(h, bf.TL, b, nk * a2, 1.0f, Ek, lda, true, a, X[k], nk * a2, false, xt);
                 // E' (a2 x b2) = (2^-e T)^T ((b nk) x a2)^T Y_k ((b nk) x b2)
                 SgemmExtra xe;
                 xe.sa = TLw(k);
@@ -173,17 +189,19 @@ void dot32_enqueue(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, 
                 sgemm<float, double>(h, En, a2, b2, 1.0f, bf.TL, a2, true, b * nk, Y[k], b2, false, xe);
                 std::swap(E, En);
             }
-            if (s < d - m) {
+            if (s < nr) {
                 fork.main();
-                const size_t k = d - 1 - s;
+                const size_t k = kr - s;
                 const size_t a = rx[k], b = ry[k], nk = n[k], a2 = rx[k + 1], b2 = ry[k + 1];
-                const float* Fk = s == 0 ? one : F;
+                const bool first = s == 0;
+                const float* Fk = first ? (st.Fr ? st.Fr : one) : F;
+                const size_t ldb = first && st.Fr ? st.ldf : b2;
                 // T (a nk x b2) = X_k (a nk x a2) 2^-e F
                 SgemmExtra xt;
-                xt.sb = s == 0 ? one_max : R(k + 1);
+                xt.sb = (first && !st.Fr) ? one_max : R(k + 1);
                 xt.amax = TRw(k);
                 xt.cmax_a = sx(k);
-                sgemm<double, float>(h, bf.TR, a * nk, b2, 1.0f, X[k], a2, false, a2, Fk, b2, false, xt);
+                sgemm<double, float>(h, bf.TR, a * nk, b2, 1.0f, X[k], a2, false, a2, Fk, ldb, false, xt);
                 // F' (a x b) = (2^-e T) (a x nk b2) Y_k^T
                 SgemmExtra xe;
                 xe.sa = TRw(k);
@@ -206,13 +224,21 @@ double dot_f32(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
                const double* const* Y) {
     XRS_REQUIRE(d >= 2 && d <= 2048, "the fp32 zipper takes 2..2048 components");
     for (size_t k = 0; k <= d; ++k) XRS_REQUIRE(rx[k] * ry[k] < (size_t(1) << 30), "fp32 zipper: rank product too large");
-    // the fused form (zip32.hip: one launch per step for both ends) where the shapes allow it; XRS_ZIP32=0 keeps
-    // this per-product form for every shape (A/B runs)
+    // zip32.hip's fused forms, opt-in (r06, one box, tools/dot32_probe.py: this per-product form 0.215 ms,
+    // XRS_ZIP32=1 -- fused front end, then these steps -- 0.219-0.225 ms, XRS_ZIP32=2 -- fused steps throughout --
+    // 0.258 ms; profiles/r06/zip32_ab_r06.txt)
     static const bool no_zip = [] {
         const char* e = std::getenv("XRS_ZIP32");
-        return e && e[0] == '0';
+        return !(e && e[0] == '1');
     }();
-    if (!no_zip && zip::applicable(d, n, rx, X, ry, Y)) return zip::dot(h, d, n, rx, X, ry, Y);
+    // XRS_ZIP32=2: the fused zipper for every step (zip32.hip; measured slower per full-rank step than the
+    // per-product launches below, kept for A/B runs)
+    static const bool all_zip = [] {
+        const char* e = std::getenv("XRS_ZIP32");
+        return e && e[0] == '2';
+    }();
+    if (all_zip && zip::applicable(d, n, rx, X, ry, Y)) return zip::dot(h, d, n, rx, X, ry, Y);
+    const bool use_front = !no_zip && zip::front_applicable(d, n, rx, X, ry, Y);
     const size_t m = d / 2;
     size_t off[7];
     Dot32Bufs b{};
@@ -221,19 +247,41 @@ double dot_f32(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
     auto f = [&](int i) { return reinterpret_cast<float*>(base + off[i]); };
     b.E0 = f(0), b.E1 = f(1), b.F0 = f(2), b.F1 = f(3), b.TL = f(4), b.TR = f(5);
     b.W = base + off[6];
-    dot32_enqueue(h, d, n, rx, X, ry, Y, b);
-    // read back the closing sum, the core maxima and the max words' values
+    dot32_init(h, b);
+    // the front end (zip32.hip: E_1 / F_{d-1} and the rank r_1 -> r_2 step of each end in fused launches) where the
+    // shapes allow it, then the per-product steps from core 2 / d - 3
+    zip::Front fr;
+    Dot32Start st;
+    if (use_front) {
+        unsigned* words = reinterpret_cast<unsigned*>(b.W + b.words_off);
+        fr.mword[0] = words + 2 * kMaxLanes;                    // L(2)
+        fr.mword[1] = words + (d + 1 + d - 2) * kMaxLanes;      // R(d - 2)
+        fr.slots = reinterpret_cast<unsigned*>(b.W + b.slots_off);
+        zip::front(h, d, n, rx, X, ry, Y, fr);
+        st.kl = 2, st.El = fr.E, st.lde = fr.lde;
+        st.kr = d - 3, st.Fr = fr.F, st.ldf = fr.ldf;
+    }
+    dot32_enqueue(h, d, n, rx, X, ry, Y, b, st);
+    // read back the closing sum, the core maxima and the max words' values (+ the front end's exponent words)
     char* hs = static_cast<char*>(h->host_scratch);
-    XRS_REQUIRE(b.back_bytes <= (size_t(1) << 16), "fp32 zipper: read-back exceeds the host scratch");
+    const size_t zoff = (b.back_bytes + 255) / 256 * 256;
+    XRS_REQUIRE(zoff + 16 * d <= (size_t(1) << 16), "fp32 zipper: read-back exceeds the host scratch");
     XRS_HIP(hipMemcpyAsync(hs, b.W, b.back_bytes, hipMemcpyDeviceToHost, h->stream));
+    if (use_front) XRS_HIP(hipMemcpyAsync(hs + zoff, fr.words, 16 * d, hipMemcpyDeviceToHost, h->stream));
     host_wait(h);
+    const int* zw = reinterpret_cast<const int*>(hs + zoff);
+    if (use_front && zip::front_words_bad(zw, d)) return tt::dot(h, d, n, rx, X, ry, Y);
     const unsigned* hc = reinterpret_cast<const unsigned*>(hs + 8 * kPairBlocks);
     const unsigned* hw = hc + 2 * d;
     // every core's max|.| in [2^-100, 2^100) or zero, else the fp64 zipper
     for (size_t c = 0; c < 2 * d; ++c) {
         const unsigned bits = hc[c];
         const int e = int((bits >> 23) & 0xff) - 127;   // floor(log2 max)
-        if (bits != 0u && (bits >= 0x7f800000u || e < -100 || e >= 100)) return tt::dot(h, d, n, rx, X, ry, Y);
+        // (the front end's step reads cores 1 and d-2 in fp32: a zero max there may be an underflowed core)
+        const size_t k = c % d;
+        const bool front_core = use_front && (k == 1 || k == d - 2);
+        if ((bits != 0u || front_core) && (bits == 0u || bits >= 0x7f800000u || e < -100 || e >= 100))
+            return tt::dot(h, d, n, rx, X, ry, Y);
     }
     // a product that left the fp32 range anyway (a max word or the closing sum not finite: products bounded
     // by (n r)^2 max|core|^2 can still overflow at rank products near the 2^30 limit): the fp64 zipper
@@ -247,11 +295,18 @@ double dot_f32(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, cons
     }
     if (!std::isfinite(v)) return tt::dot(h, d, n, rx, X, ry, Y);
     // the powers of two the products scaled their normalised operands by: left E_k (k = 1..m-1; E_0 = [1]:
-    // 2^-1) and T of cores 0..m-1, right F_k (k = m+1..d-1; F_d = [1]: 2^-1) and T of cores m..d-1
-    int e = 2 * pow2_exponent(0x3f800000u);
-    for (size_t k = 1; k < m; ++k) e += pow2_exponent(hw[k]);
-    for (size_t k = m + 1; k < d; ++k) e += pow2_exponent(hw[d + 1 + k]);
-    for (size_t k = 0; k < d; ++k) e += pow2_exponent(hw[(k < m ? 2 * d + 2 : 3 * d + 2) + k]);
+    // 2^-1) and T of cores 0..m-1, right F_k (k = m+1..d-1; F_d = [1]: 2^-1) and T of cores m..d-1; with the front
+    // end: its own exponents for cores 0, 1 / d-1, d-2, then the words from E_2 / T of core 2 (F_{d-2} / core d-3) on
+    int e = 0;
+    const size_t kl = use_front ? 2 : 1, kr = use_front ? d - 1 : d;   // (words L(kl..m-1), R(m+1..kr-1))
+    if (use_front) e += zip::front_exponent(zw, d, 0) + zip::front_exponent(zw, d, 1);
+    else e += 2 * pow2_exponent(0x3f800000u);
+    for (size_t k = kl; k < m; ++k) e += pow2_exponent(hw[k]);
+    for (size_t k = m + 1; k < kr; ++k) e += pow2_exponent(hw[d + 1 + k]);
+    for (size_t k = 0; k < d; ++k) {
+        if (use_front && (k < 2 || k + 2 >= d)) continue;
+        e += pow2_exponent(hw[(k < m ? 2 * d + 2 : 3 * d + 2) + k]);
+    }
     return std::ldexp(v, e);
 }
 

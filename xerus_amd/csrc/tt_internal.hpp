@@ -19,5 +19,25 @@ bool applicable(size_t d, const size_t* n, const size_t* rx, const double* const
                 const double* const* Y);
 double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
            const double* const* Y);
+// The front end alone (E_1 / F_{d-1} and one step per end) for dot32.hip's per-product steps: E_2 and F_{d-2} in fp32
+// (row strides lde / ldf), their max words written into mword[0] / mword[1], the cores' maxima into the caller's
+// slot arrays (kCmaxSlots words per core: X_k at k, Y_k at d + k), and 4d exponent words at `words` (device; the
+// caller reads them back and passes them to front_exponent / front_words_bad). mem holds the buffers: keep it until
+// the caller's launches are enqueued.
+struct Front {
+    unsigned* mword[2] = {nullptr, nullptr};
+    unsigned* slots = nullptr;
+    const float* E = nullptr;
+    const float* F = nullptr;
+    size_t lde = 0, ldf = 0;
+    int* words = nullptr;
+    DevBuf mem;
+};
+bool front_applicable(size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+                      const double* const* Y);
+void front(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y, Front& fr);
+int front_exponent(const int* hw, size_t d, int end);
+bool front_words_bad(const int* hw, size_t d);
 }  // namespace zip
 }  // namespace xrs

@@ -211,26 +211,37 @@ __device__ unsigned long long* g_zip_stamps = nullptr;
                                                __builtin_amdgcn_s_getreg((31 << 11) | 4);                    \
     }
 
-constexpr int kLdT = 260;   // T^T row stride in LDS (floats): 4-bank shift per row, conflict-free float4 reads
 
-// FULL: every row / column of the unit is inside the true ranks (M1 = K2 = 256, N1 % 32 == 0, N2 == N2p): no masks
-template <bool E64, bool RIGHT, int PD, int NC, bool FULL>
-__device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const int blk, float* ltt, double* red) {
+// FULL: every row / column of the unit is inside the true ranks (K1r = K1, M1r = M1, N1 % 32 == 0, N2 == N2p): no
+// masks or clamps. KH: the unit's share of T's rows (= the second product's K): 1 all M1 rows; 2 half h of them
+// (twice the units, each half the work -- 640 instead of 320 at rank 256, so the CUs that hold one unit more than
+// the others carry half the excess). Phase 1 waves: KH 1: wave w owns rows 64 w + [0, 64) and the unit's 32
+// columns (2 col-blocks); KH 2: rows h M1/2 + 64 (w & 1) + [0, 64), columns 16 (w >> 1) + [0, 16) (1 col-block).
+template <bool E64, bool RIGHT, int PD, int NC1, int NC2, bool FULL, int KH, int BR, int PD1 = PD>
+__device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const int blk, const int h, float* ltt, double* red) {
+    constexpr int RG = KH == 1 ? 4 : 2;  // waves per column group (phase 1)
+    constexpr int CW = BR * RG / 4;      // phase-1 columns per wave
+    constexpr int CB = CW / 16;          // phase-1 col-blocks per wave
+    static_assert(CB == 1 || CB == 2, "16 or 32 phase-1 columns per wave");
+    constexpr int RB2 = BR / 16;         // phase-2 row-blocks
+    constexpr int LDT = 256 / KH + 4;    // T^T row stride in LDS (floats): a 4-bank shift per row
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
     const int M1 = p.M1, N1 = p.N1, N2 = p.N2;
+    const int mh = M1 / KH;              // rows of T in this unit (K of phase 2)
     const double* __restrict__ X = p.X + size_t(i) * p.xi;
-    const double* __restrict__ Y = p.Y + size_t(i) * p.yi;
+    const double* __restrict__ Y = p.Y + size_t(i) * p.yi + size_t(h) * mh * p.yk;
     // max|.| of the cores as converted to fp32 (one v_max_f32 per element): a core above the fp32 range shows as
     // inf, one whose max lies below 2^-100 as a small or zero max -- the host sends both to the fp64 zipper
     float vmx = 0.0f, vmy = 0.0f;
 
-    // ---- phase 1: T rows [64 w, 64 w + 64) of the wave (row-block q <-> rows 64 w + 4 r + q), columns
-    // blk*32 + 2 r + q (col-block q in {0, 1}); K1 in 16-deep chunks, lane group g takes k = 4 g + j (j = MFMA)
-    const int rowbase = 64 * w;
+    // ---- phase 1: T rows of the wave (row-block a <-> rows rowbase + 4 r + a), columns c1 (+ q); K1 in 16-deep
+    // chunks, lane group g takes k = 4 g + j (j = MFMA)
+    const int rg = w % RG, cg = w / RG;
+    const int rowbase = h * mh + 64 * rg;
     const bool rows_ok = FULL || rowbase + 4 * r < M1;
     const int erow = rows_ok ? rowbase + 4 * r : 0;
-    const int c1 = blk * 32 + 2 * r;
+    const int c1 = blk * BR + cg * CW + (CB == 2 ? 2 * r : r);
     const bool cols1_ok = FULL || c1 < N1;
     const int xcol = cols1_ok ? c1 : 0;
     const int C1 = p.K1 / 16;
@@ -242,13 +253,17 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
     struct R1 {
         f4 e[4];      // E[k][erow .. +3] for j = 0..3 (fp32 E)
         d2 e64[4][2]; // (fp64 E)
-        d2 x[4];      // LEFT: x[j] = Xs(k_j, c1 .. c1+1); RIGHT: x[2q + h] = Xs(k0 + 2h .. +1, c1 + q)
+        d2 x[4];      // LEFT: x[j] = Xs(k_j, c1 .. c1 + CB - 1); RIGHT: x[2q + hh] = Xs(k0 + 2hh .. +1, c1 + q)
     };
-    R1 ring1[PD];
-    float ea[2][4][4], xb[2][4][2];   // converted operands, two sets
+    R1 ring1[PD1];
+    float ea[2][4][4], xb[2][4][CB];   // converted operands, two sets
     // FULL: per-lane base addresses once, a wave-uniform offset per chunk (no clamps: every row is real)
     const float* eb = static_cast<const float*>(p.E) + size_t(4 * g) * M1 + erow;
     const double* xb0 = RIGHT ? X + size_t(xcol) * p.xc + 4 * g : X + size_t(4 * g) * p.xk + xcol;
+    auto load_x_left = [&](R1& s, int j, const double* xp) {
+        if constexpr (CB == 2) s.x[j] = *reinterpret_cast<const d2*>(xp);
+        else s.x[j][0] = *xp;
+    };
     auto load1 = [&](auto slot_c, int c) {
         R1& s = ring1[decltype(slot_c)::value];
         c = min(c, C1 - 1);
@@ -259,13 +274,13 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
             if constexpr (!RIGHT) {
                 const double* x = xb0 + size_t(16 * c) * p.xk;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) s.x[j] = *reinterpret_cast<const d2*>(x + size_t(j) * p.xk);
+                for (int j = 0; j < 4; ++j) load_x_left(s, j, x + size_t(j) * p.xk);
             } else {
                 const double* x = xb0 + 16 * c;
 #pragma unroll
-                for (int q = 0; q < 2; ++q)
+                for (int q = 0; q < CB; ++q)
 #pragma unroll
-                    for (int h = 0; h < 2; ++h) s.x[2 * q + h] = *reinterpret_cast<const d2*>(x + size_t(q) * p.xc + 2 * h);
+                    for (int hh = 0; hh < 2; ++hh) s.x[2 * q + hh] = *reinterpret_cast<const d2*>(x + size_t(q) * p.xc + 2 * hh);
             }
             return;
         }
@@ -282,14 +297,14 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
         }
         if constexpr (!RIGHT) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s.x[j] = *reinterpret_cast<const d2*>(X + size_t(min(k0 + j, kx)) * p.xk + xcol);
+            for (int j = 0; j < 4; ++j) load_x_left(s, j, X + size_t(min(k0 + j, kx)) * p.xk + xcol);
         } else {
             // (K1r even: a pair starting inside the real rows lies inside them)
 #pragma unroll
-            for (int q = 0; q < 2; ++q)
+            for (int q = 0; q < CB; ++q)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)
-                    s.x[2 * q + h] = *reinterpret_cast<const d2*>(X + size_t(xcol + q) * p.xc + min(k0 + 2 * h, kx - 1));
+                for (int hh = 0; hh < 2; ++hh)
+                    s.x[2 * q + hh] = *reinterpret_cast<const d2*>(X + size_t(xcol + q) * p.xc + min(k0 + 2 * hh, kx - 1));
         }
     };
     auto conv1 = [&](auto slot_c, auto set_c, int) {
@@ -305,7 +320,7 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
                 ea[S][j][q] = rows_ok ? v : 0.0f;
             }
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
+            for (int q = 0; q < CB; ++q) {
                 double v;
                 if constexpr (!RIGHT) v = s.x[j][q];
                 else v = s.x[2 * q + (j >> 1)][j & 1];
@@ -316,11 +331,11 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
         }
         asm volatile("" : "+v"(vmx));   // the running max stays per chunk (no deferred max tree over the loop)
     };
-    f4 acc1[4][2];
+    f4 acc1[4][CB];
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc1[a][b] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int b = 0; b < CB; ++b) acc1[a][b] = f4{0.f, 0.f, 0.f, 0.f};
     auto mma1 = [&](auto set_c, int) {
         constexpr int S = decltype(set_c)::value;
 #pragma unroll
@@ -328,26 +343,26 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
 #pragma unroll
             for (int a = 0; a < 4; ++a)
 #pragma unroll
-                for (int b = 0; b < 2; ++b) acc1[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(ea[S][j][a], xb[S][j][b], acc1[a][b], 0, 0, 0);
+                for (int b = 0; b < CB; ++b) acc1[a][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(ea[S][j][a], xb[S][j][b], acc1[a][b], 0, 0, 0);
     };
     XRS_ZIP_STAMP(0)
     if (rowbase < M1) {
-        k_chain_prologue<PD>(load1);
-        k_chain<NC, PD>(C1, load1, conv1, mma1);
+        k_chain_prologue<PD1>(load1);
+        k_chain<NC1, PD1>(C1, load1, conv1, mma1);
     }
     __builtin_amdgcn_sched_barrier(0);
     XRS_ZIP_STAMP(1)
 
-    // ---- phase 2 operands start loading now (they do not depend on T): Ys(k, colbase + 4 r + q), wave
-    // columns [64 w, 64 w + 64), K = M1
+    // ---- phase 2 operands start loading now (they do not depend on T): Ys(h mh + k, colbase + 4 r + q), wave
+    // columns [64 w, 64 w + 64), K = mh
     const int colbase = 64 * w;
     const int c2 = colbase + 4 * r;
     const bool cols2_ok = FULL || c2 < N2;
     const int ycol = cols2_ok ? c2 : 0;
-    const int C2 = M1 / 16;
-    const int ky = p.M1r - 1;
+    const int C2 = mh / 16;
+    const int ky = p.M1r - 1 - h * mh;   // last real row of this unit's Ys rows
     struct R2 {
-        d2 y[8];   // LEFT: y[2j + h] = Ys(k_j, ycol + 2h .. +1); RIGHT: y[2q + h] = Ys(k0 + 2h .. +1, ycol + q)
+        d2 y[8];   // LEFT: y[2j + hh] = Ys(k_j, ycol + 2hh .. +1); RIGHT: y[2q + hh] = Ys(k0 + 2hh .. +1, ycol + q)
     };
     R2 ring2[PD];
     float yb[2][4][4];
@@ -409,72 +424,74 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
     const bool wave2 = colbase < p.N2p;
     if (wave2) k_chain_prologue<PD>(load2);   // in flight across T's reduction and the barrier
 
-    // ---- T's exponent (this unit's own), T^T into LDS scaled by 2^-t: lane (n, mg) holds block (a, b) reg e at
-    // row 64 w + 4 (4 mg + e) + a, column 2 n + b
-    double tm = 0.0;
+    // ---- T's exponent (this unit's own), T^T into LDS scaled by 2^-t: lane (n, mg) holds block (a, q) reg e at
+    // T row rowbase + 4 (4 mg + e) + a = local k 64 rg + 16 mg + 4 e + a, column (KH 1) 2 n + q / (KH 2) 16 cg + n
+    float tmf = 0.0f;
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < CB; ++b)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) tm = fmax(tm, double(fabsf(acc1[a][b][e])));
-    tm = block_max(tm, red);
+            for (int e = 0; e < 4; ++e) tmf = fmaxf(tmf, fabsf(acc1[a][b][e]));
+    const double tm = block_max(double(tmf), red);
     const int tw = exp_word(tm);
     const int te = f32_exp(tw);
     const float ts = pow2f(-te);
     if (rowbase < M1) {
         const int n = lane & 15, mg = lane >> 4;
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < CB; ++b)
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const f4 v = f4{acc1[0][b][e], acc1[1][b][e], acc1[2][b][e], acc1[3][b][e]} * ts;
-                *reinterpret_cast<f4*>(ltt + (2 * n + b) * kLdT + rowbase + 16 * mg + 4 * e) = v;
+                const int col = cg * CW + (CB == 2 ? 2 * n + b : n);
+                *reinterpret_cast<f4*>(ltt + col * LDT + 64 * rg + 16 * mg + 4 * e) = v;
             }
     }
+    const int unit = (i * p.nblk + blk) * KH + h;
     if (tid == 0) {
-        p.texp[i * p.nblk + blk] = tw == 0 ? 0 : te + kBias;
+        p.texp[unit] = tw == 0 ? 0 : te + kBias;
         atomicMax(p.tmax, tw == 0 ? 0 : te + kBias);
     }
     __syncthreads();
     XRS_ZIP_STAMP(2)
 
-    // ---- phase 2: P (32 x N2p) = (T^T) Ys; row-block a in {0, 1}: rows 16 a + r; col-block q: columns c2 + q
-    f4 acc2[2][4];
+    // ---- phase 2: P (BR x N2p) = (T^T) Ys; row-block a < RB2: rows 16 a + r; col-block q: columns c2 + q
+    f4 acc2[RB2][4];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < RB2; ++a)
 #pragma unroll
         for (int b = 0; b < 4; ++b) acc2[a][b] = f4{0.f, 0.f, 0.f, 0.f};
     auto mma2 = [&](auto set_c, int c) {
         constexpr int S = decltype(set_c)::value;
         const int k0 = 16 * c + 4 * g;
-        f4 ta[2];
+        f4 ta[RB2];
 #pragma unroll
-        for (int a = 0; a < 2; ++a) ta[a] = *reinterpret_cast<const f4*>(ltt + (16 * a + r) * kLdT + k0);
+        for (int a = 0; a < RB2; ++a) ta[a] = *reinterpret_cast<const f4*>(ltt + (16 * a + r) * LDT + k0);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < RB2; ++a)
 #pragma unroll
                 for (int q = 0; q < 4; ++q) acc2[a][q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ta[a][j], yb[S][j][q], acc2[a][q], 0, 0, 0);
     };
     if (wave2) {
-        k_chain<NC, PD>(C2, load2, conv2, mma2);
+        k_chain<NC2, PD>(C2, load2, conv2, mma2);
         XRS_ZIP_STAMP(3)
         // P rows 16 a + 4 mg + e of this unit, columns colbase + 4 n .. +3 (zeros outside N1 x N2)
         const int n = lane & 15, mg = lane >> 4;
         const int col = colbase + 4 * n;
-        float* out = p.slab + (size_t(i) * p.nblk + blk) * 32 * size_t(p.N2p);
+        float* out = p.slab + size_t(unit) * BR * size_t(p.N2p);
         if (col < p.N2p) {
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < RB2; ++a)
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
                     *reinterpret_cast<f4*>(out + size_t(16 * a + 4 * mg + e) * p.N2p + col) =
                         f4{acc2[a][0][e], acc2[a][1][e], acc2[a][2][e], acc2[a][3][e]};
         }
     }
-    const unsigned slot = unsigned(i * p.nblk + blk) % unsigned(kCmaxSlots);
+    const unsigned slot = unsigned(unit) % unsigned(kCmaxSlots);
     wave_max_slot_f(p.cx + slot, vmx);
     wave_max_slot_f(p.cy + slot, vmy);
     XRS_ZIP_STAMP(4)
@@ -482,20 +499,18 @@ __device__ __forceinline__ void zstep_unit(const StepEnd& p, const int i, const 
 
 // units are dealt to the XCDs in contiguous ranges (workgroups go to the 8 XCDs round-robin by dispatch
 // order): the units of one (end, i) -- which read the same Y_k[:, i, :] -- run in one L2
-template <bool E64, int PD, int NC, bool FULL>
+template <bool E64, int PD, int NC1, int NC2, bool FULL, int KH, int BR, int PD1 = PD>
 __global__ void __launch_bounds__(256, 2) k_zstep(const StepArgs args) {
-    __shared__ float ltt[32 * kLdT];
+    __shared__ float ltt[BR * (256 / KH + 4)];
     __shared__ double red[8];
     int u = int(blockIdx.x);
     if (args.units % 8 == 0) u = (u & 7) * (args.units / 8) + (u >> 3);
-    if (u < args.units0) {
-        const StepEnd& p = args.e[0];
-        zstep_unit<E64, false, PD, NC, FULL>(p, u / p.nblk, u % p.nblk, ltt, red);
-    } else {
-        const StepEnd& p = args.e[1];
-        u -= args.units0;
-        zstep_unit<E64, true, PD, NC, FULL>(p, u / p.nblk, u % p.nblk, ltt, red);
-    }
+    const bool left = u < args.units0;
+    const StepEnd& p = args.e[left ? 0 : 1];
+    if (!left) u -= args.units0;
+    const int h = u % KH, q = u / KH;
+    if (left) zstep_unit<E64, false, PD, NC1, NC2, FULL, KH, BR, PD1>(p, q / p.nblk, q % p.nblk, h, ltt, red);
+    else zstep_unit<E64, true, PD, NC1, NC2, FULL, KH, BR, PD1>(p, q / p.nblk, q % p.nblk, h, ltt, red);
 }
 
 // ------------------------------------------------------------------------------------------------ reduce
@@ -506,7 +521,8 @@ struct RedEnd {
     const int* tmax;
     float* out;
     int* eword;        // exponent word of max|out|
-    int n, nblk, N1p, N2p;
+    unsigned* mword;   // optional: max word (float bits, kMaxLanes lanes) of max|out| (dot32.hip's steps read it)
+    int n, nblk, N1p, N2p, kh, br;
     int blocks;
 };
 struct RedArgs {
@@ -523,35 +539,37 @@ __global__ void __launch_bounds__(kRedT) k_zreduce(const RedArgs args) {
     const int per_row = p.N2p / 4;
     const bool ok = q < p.N1p * per_row;
     const int row = ok ? q / per_row : 0, col = ok ? (q % per_row) * 4 : 0;
-    const int blk = row >> 5, rr = row & 31;
+    const int blk = row / p.br, rr = row % p.br;
     const int tm = *p.tmax;
     f4 s = f4{0.f, 0.f, 0.f, 0.f};
     if (ok) {
-        const float* src = p.slab + (size_t(blk) * 32 + rr) * p.N2p + col;
-        const size_t stride = size_t(p.nblk) * 32 * p.N2p;
-        int i = 0;
-        for (; i + 4 <= p.n; i += 4) {   // four slabs per round trip, summed in slice order
-            f4 v[4];
-            float sc[4];
+        // slab of (i, blk, h): ((i nblk + blk) kh + h); summed over (i, h) in that order. The slabs were written by
+        // units on every XCD: loads of up to kRedG slabs in flight per round trip
+        const float* src = p.slab + (size_t(blk) * p.kh * p.br + rr) * p.N2p + col;
+        const size_t stride_i = size_t(p.nblk) * p.kh * p.br * p.N2p, stride_h = size_t(p.br) * p.N2p;
+        const int ns = p.n * p.kh;
+        constexpr int kRedG = 20;
+        for (int s0 = 0; s0 < ns; s0 += kRedG) {
+            f4 v[kRedG];
+            float sc[kRedG];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                v[u] = *reinterpret_cast<const f4*>(src + size_t(i + u) * stride);
-                const int tw = p.texp[(i + u) * p.nblk + blk];
+            for (int u = 0; u < kRedG; ++u) {
+                const int sl = min(s0 + u, ns - 1), i = sl / p.kh, hh = sl % p.kh;
+                v[u] = *reinterpret_cast<const f4*>(src + size_t(i) * stride_i + size_t(hh) * stride_h);
+                const int tw = p.texp[(i * p.nblk + blk) * p.kh + hh];
                 const int de = tw == 0 ? -1000 : tw - tm;
-                sc[u] = de < -126 ? 0.0f : pow2f(de);
+                sc[u] = (de < -126 || s0 + u >= ns) ? 0.0f : pow2f(de);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) s += sc[u] * v[u];
-        }
-        for (; i < p.n; ++i) {
-            const int tw = p.texp[i * p.nblk + blk];
-            const int de = tw == 0 ? -1000 : tw - tm;
-            s += (de < -126 ? 0.0f : pow2f(de)) * *reinterpret_cast<const f4*>(src + size_t(i) * stride);
+            for (int u = 0; u < kRedG; ++u) s += sc[u] * v[u];
         }
         *reinterpret_cast<f4*>(p.out + size_t(row) * p.N2p + col) = s;
     }
     const double m = block_max(ok ? double(fmaxf(fmaxf(fabsf(s[0]), fabsf(s[1])), fmaxf(fabsf(s[2]), fabsf(s[3])))) : 0.0, red);
-    if (threadIdx.x == 0) atomicMax(p.eword, exp_word(m));
+    if (threadIdx.x == 0) {
+        atomicMax(p.eword, exp_word(m));
+        if (p.mword) atomicMax(p.mword + b % kMaxLanes, __float_as_uint(float(m)));
+    }
 }
 
 // ------------------------------------------------------------------------------------------------ finish
@@ -602,10 +620,14 @@ bool applicable(size_t d, const size_t* n, const size_t* rx, const double* const
     return true;
 }
 
-double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
-           const double* const* Y) {
+namespace {
+// fr == null: the whole product (returns it). fr != null: the front end only -- E_1 / F_{d-1} and the first step
+// of each end -- with the environments E_2 / F_{d-2} (fp32, padded, max words into fr->mword) and the exponent
+// words left for the caller (returns 0); the caller's slot arrays receive the cores' maxima.
+double run(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y, Front* fr) {
     const size_t m = d / 2;
-    const size_t sl = m - 1, sr = d - 1 - m;   // steps per end (cores 1..m-1 / d-2..m)
+    const size_t sl = fr ? 1 : m - 1, sr = fr ? 1 : d - 1 - m;   // steps per end (cores 1..m-1 / d-2..m)
     const size_t steps = std::max(sl, sr);
     auto p32 = [](size_t x) { return (x + 31) / 32 * 32; };
     auto up = [](size_t x) { return (x + 255) / 256 * 256; };
@@ -613,8 +635,8 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
     size_t slab_f = 0, tex = 1, env = 1;
     for (size_t k = 1; k + 1 < d; ++k) {
         const size_t nb = (std::max(rx[k], rx[k + 1]) + 31) / 32;
-        slab_f = std::max(slab_f, n[k] * nb * 32 * p32(std::max(ry[k], ry[k + 1])));
-        tex = std::max(tex, n[k] * nb);
+        slab_f = std::max(slab_f, 2 * n[k] * nb * 32 * p32(std::max(ry[k], ry[k + 1])));   // (2: KH up to 2)
+        tex = std::max(tex, 2 * n[k] * nb);
     }
     for (size_t k = 1; k < d; ++k) env = std::max(env, p32(rx[k]) * p32(ry[k]));
     const size_t s0 = p32(rx[1]) * p32(ry[1]), s1 = p32(rx[d - 1]) * p32(ry[d - 1]);
@@ -639,7 +661,7 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
     float* slab[2] = {reinterpret_cast<float*>(base + o_slab), reinterpret_cast<float*>(base + o_slab + up(4 * slab_f))};
     double* part = reinterpret_cast<double*>(base + o_part);
     int* words = reinterpret_cast<int*>(base + o_words);
-    unsigned* slots = reinterpret_cast<unsigned*>(base + o_slots);
+    unsigned* slots = fr ? fr->slots : reinterpret_cast<unsigned*>(base + o_slots);
     int* texb[2] = {reinterpret_cast<int*>(base + o_tex), reinterpret_cast<int*>(base + o_tex + up(4 * tex * nst))};
     auto ew = [&](int e, size_t k) { return words + e * d + k; };
     auto tw = [&](int e, size_t k) { return words + 2 * d + e * d + k; };
@@ -647,8 +669,8 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
     auto sx = [&](size_t k) { return slots + k * kCmaxSlots; };
     auto sy = [&](size_t k) { return slots + (d + k) * kCmaxSlots; };
 
-    {   // words, core-max slots (zeroed: the kernels atomicMax into them)
-        const size_t zw = (o_tex - o_words) / 4;
+    {   // words, core-max slots (zeroed: the kernels atomicMax into them; a front end's slots are the caller's)
+        const size_t zw = ((fr ? o_slots : o_tex) - o_words) / 4;
         hipLaunchKernelGGL(k_zinit, dim3(256), dim3(256), 0, h->stream, reinterpret_cast<unsigned*>(words), zw);
         check_launch("k_zinit");
     }
@@ -667,7 +689,7 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
     DevBuf stamp_buf;
     if (stamps) {
         size_t mx = 1;
-        for (size_t k = 0; k < d; ++k) mx = std::max(mx, 2 * n[k] * ((std::max(rx[k], rx[k + 1]) + 31) / 32));
+        for (size_t k = 0; k < d; ++k) mx = std::max(mx, 4 * n[k] * ((std::max(rx[k], rx[k + 1]) + 31) / 32));
         stamp_buf = DevBuf(h, mx * 64);
         unsigned long long* sp = stamp_buf.as<unsigned long long>();
         XRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_zip_stamps), &sp, sizeof(sp), 0, hipMemcpyHostToDevice, h->stream));
@@ -708,7 +730,8 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
             p.nblk = (p.N1 + 31) / 32;
             units[slot] = p.n * p.nblk;
             RedEnd& q = ra.e[slot];
-            q = RedEnd{slab[e], p.texp, p.tmax, nxt[e], ew(e, eout), p.n, p.nblk, 32 * p.nblk, p.N2p, 0};
+            q = RedEnd{slab[e], p.texp, p.tmax, nxt[e], ew(e, eout), fr ? fr->mword[e] : nullptr, p.n, p.nblk, 32 * p.nblk,
+                       p.N2p, 1, 32, 0};
             q.blocks = (q.N1p * q.N2p / 4 + kRedT - 1) / kRedT;
             rblocks[slot] = q.blocks;
             ++slot;
@@ -734,8 +757,8 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
                 if ((p.K1 / 16) % 4 || (p.M1 / 16) % 4) all4 = false;
             }
             KernelTimer timer(h, XRS_KFAM_GEMM, flops, bytes, true);
-            // K of both products (K1, M1) 256 at every end of the launch: the fully unrolled chains, and no masks
-            // when every unit lies inside the true ranks
+            // K of both products (K1, M1) 256 at every end of the launch: the fully unrolled chains, half units
+            // (KH 2), and no masks when every unit lies inside the true ranks
             bool full = true, whole = true;
             for (int e = 0; e < 2; ++e) {
                 if (!units[e]) continue;
@@ -744,23 +767,43 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
                 if (p.K1r != 256 || p.M1r != 256 || p.N1 % 32 || p.N2 != p.N2p) whole = false;
             }
             const bool e64 = s == 0;
-#define XRS_ZSTEP(E64_, PD_, NC_, FULL_) \
-    hipExtLaunchKernelGGL((k_zstep<E64_, PD_, NC_, FULL_>), dim3(sa.units), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0, sa)
+            // unit geometry: full steps KH 2 (T rows in halves); 64-row units where every end's N1 allows them
+            bool br64 = full;
+            for (int e = 0; e < 2; ++e)
+                if (units[e] && sa.e[e].N1 % 64) br64 = false;
+            const int kh = (!e64 && full) ? 2 : 1, br = br64 ? 64 : 32;
+            for (int e = 0; e < 2; ++e) {
+                if (!units[e]) continue;
+                StepEnd& p = sa.e[e];
+                p.nblk = (p.N1 + br - 1) / br;
+                units[e] = p.n * p.nblk;
+                ra.e[e].nblk = p.nblk;
+                ra.e[e].kh = kh;
+                ra.e[e].br = br;
+            }
+            sa.units0 = units[0] * kh;
+            sa.units = (units[0] + units[1]) * kh;
+            const unsigned grid = unsigned(sa.units);
+#define XRS_ZSTEP(E64_, PD_, NC1_, NC2_, FULL_, KH_, BR_, ...) \
+    hipExtLaunchKernelGGL((k_zstep<E64_, PD_, NC1_, NC2_, FULL_, KH_, BR_ __VA_OPT__(,) __VA_ARGS__>), dim3(grid), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0, sa)
             if (e64) {
-                XRS_ZSTEP(true, 2, 0, false);   // (the fp64 ring of 4 spills; the first step is short)
+                XRS_ZSTEP(true, 2, 0, 0, false, 1, 32);   // (the fp64 ring of 4 spills; the first step is short)
+            } else if (br64) {
+                if (whole) XRS_ZSTEP(false, 3, 16, 8, true, 2, 64, 5);
+                else XRS_ZSTEP(false, 3, 16, 8, false, 2, 64, 5);
             } else {
-                if (full && whole) XRS_ZSTEP(false, 4, 16, true);
-                else if (full) XRS_ZSTEP(false, 4, 16, false);
-                else if (all4) XRS_ZSTEP(false, 4, 0, false);
-                else XRS_ZSTEP(false, 2, 0, false);
+                if (full && whole) XRS_ZSTEP(false, 4, 16, 8, true, 2, 32);
+                else if (full) XRS_ZSTEP(false, 4, 16, 8, false, 2, 32);
+                else if (all4) XRS_ZSTEP(false, 4, 0, 0, false, 1, 32);
+                else XRS_ZSTEP(false, 2, 0, 0, false, 1, 32);
             }
 #undef XRS_ZSTEP
             check_launch("k_zstep");
             if (stamps) {   // one line per workgroup on stderr: step, wg, xcc<<32|hwid, stamps 0..4
-                std::vector<unsigned long long> hv(size_t(sa.units) * 8);
+                std::vector<unsigned long long> hv(size_t(grid) * 8);
                 XRS_HIP(hipMemcpyAsync(hv.data(), stamp_buf.d(), hv.size() * 8, hipMemcpyDeviceToHost, h->stream));
                 host_wait(h);
-                for (int wg = 0; wg < sa.units; ++wg) {
+                for (int wg = 0; wg < int(grid); ++wg) {
                     const unsigned long long* q = hv.data() + 8 * wg;
                     std::fprintf(stderr, "[zip stamps] %zu %d %llu %llu %llu %llu %llu %llu\n", s, wg, q[7], q[0], q[1], q[2], q[3], q[4]);
                 }
@@ -771,6 +814,15 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
         check_launch("k_zreduce");
         for (int e = 0; e < 2; ++e)
             if (s < (e == 0 ? sl : sr)) cur[e] = nxt[e];
+    }
+    if (fr) {   // the environments after one step per end, the words the caller reads back with its own
+        fr->E = static_cast<const float*>(cur[0]);
+        fr->lde = p32(ry[2]);
+        fr->F = static_cast<const float*>(cur[1]);
+        fr->ldf = p32(ry[d - 2]);
+        fr->words = words;
+        fr->mem = std::move(mem);
+        return 0.0;
     }
     // ---- closing at edge m: E_m (left) and F_m (right), both p32(rx[m]) x p32(ry[m]) (fp64 if an end had no step)
     const int nm = int(p32(rx[m]) * p32(ry[m]));
@@ -819,6 +871,36 @@ double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const do
         }
     }
     return std::ldexp(v, g);
+}
+
+}  // namespace
+
+double dot(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y) {
+    return run(h, d, n, rx, X, ry, Y, nullptr);
+}
+
+bool front_applicable(size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+                      const double* const* Y) {
+    return d >= 6 && applicable(d, n, rx, X, ry, Y);
+}
+
+void front(xrs_handle_t h, size_t d, const size_t* n, const size_t* rx, const double* const* X, const size_t* ry,
+           const double* const* Y, Front& fr) {
+    run(h, d, n, rx, X, ry, Y, &fr);
+}
+
+int front_exponent(const int* hw, size_t d, int end) {
+    // the first step's input scale (the fp64 start environment: unclamped) and its tmax (zip32 word layout)
+    const size_t ein = end == 0 ? 1 : d - 1, eout = end == 0 ? 2 : d - 2;
+    const int uw = hw[end * d + ein], t = hw[2 * d + end * d + eout];
+    return (uw == 0 ? 0 : uw - kBias) + (t == 0 ? 0 : t - kBias);
+}
+
+bool front_words_bad(const int* hw, size_t d) {
+    for (size_t i = 0; i < 4 * d; ++i)
+        if (hw[i] >= kBad) return true;
+    return false;
 }
 
 }  // namespace zip
