@@ -79,7 +79,7 @@ def random_cores(xe, dims, ranks, seed):
 
 def load_traffic():
     """HBM bytes per GEMM launch from the committed rocprofv3 PMC pass of this bench (or None)."""
-    for tag in ("r05", "r04", "r03", "r02"):   # the newest committed pass
+    for tag in ("r06", "r05", "r04", "r03", "r02"):   # the newest committed pass
         p = os.path.join(ROOT, "profiles", tag, "pmc_traffic.json")
         if os.path.exists(p):
             break
@@ -604,9 +604,9 @@ def main():
     # from the sequential step (<x,y> waited for before the round starts), where a launch does not share
     # the chip with the other operation's kernels; the overlapped step's per-launch figure is reported
     # beside it (its launch durations include that sharing).
-    def events_pass(fn):
+    def events_pass(fn, mask=capi.KFAM_GEMM):
         barrier()
-        h.prof_begin(capi.KFAM_GEMM)
+        h.prof_begin(mask)
         t0 = time.perf_counter()
         for _ in range(args.steps):
             fn()
@@ -616,6 +616,8 @@ def main():
 
     prof, elapsed_ev = events_pass(step_seq)
     prof_ov, elapsed_ev_ov = events_pass(step) if step is not step_seq else (prof, elapsed_ev)
+    # the separate split-K reduce launches that complete some of those GEMMs (k_splitk_reduce*), same steps
+    prof_red, _ = events_pass(step_seq, capi.KFAM_SPLITK)
 
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -666,6 +668,15 @@ def main():
                             "rocprofv3 kernel trace reports; marker events around a launch add its ~6 us dispatch latency), "
                             "so the per-launch durations agree with a kernel trace of the same pass (tools/roofline_from_trace.py)"),
             "events_pass_ms_per_step": round(elapsed_ev / args.steps * 1e3, 4),
+            "incl_splitk_reduce": {
+                "achieved": round(prof["flops"] / ((prof["ms"] + prof_red["ms"]) * 1e-3) / 1e12, 3) if prof["ms"] > 0 else 0.0,
+                "frac": round(prof["flops"] / ((prof["ms"] + prof_red["ms"]) * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4)
+                if prof["ms"] > 0 else 0.0,
+                "reduce_launches_per_step": prof_red["launches"] / args.steps,
+                "reduce_us_per_launch": round(prof_red["ms"] / max(1, prof_red["launches"]) * 1e3, 3),
+                "note": "the GEMM family's flops over the GEMM launches' AND the separate split-K reduce launches' summed "
+                        "durations (same sequential steps, reduce launches timed in a pass of their own)",
+            },
             "algorithmic_flops_per_launch": prof["flops"] / launches,
             "algorithmic_bytes_per_launch": prof["bytes"] / launches,
             "chip_level": {

@@ -321,6 +321,7 @@ int xrs_tt_dot_sharded(xrs_handle_t handle, double* result, size_t d, const size
 #define XRS_KFAM_QR 4u
 #define XRS_KFAM_SVD 8u
 #define XRS_KFAM_ELEMWISE 16u
+#define XRS_KFAM_SPLITK 32u   /* the fp64 GEMMs' separate split-K reduce launches (k_splitk_reduce*) */
 int xrs_prof_begin(xrs_handle_t handle, uint32_t family_mask);
 /** Stops instrumentation, synchronises and returns (launches, total kernel milliseconds,
  *  algorithmic flops, algorithmic bytes) of the instrumented launches. */

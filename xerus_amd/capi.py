@@ -94,7 +94,7 @@ SIGNATURES = {
                                C.POINTER(C.c_double)]),
 }
 
-KFAM_GEMM, KFAM_PERMUTE, KFAM_QR, KFAM_SVD, KFAM_ELEMWISE = 1, 2, 4, 8, 16
+KFAM_GEMM, KFAM_PERMUTE, KFAM_QR, KFAM_SVD, KFAM_ELEMWISE, KFAM_SPLITK = 1, 2, 4, 8, 16, 32
 ROUND_PATHS = {0: None, 1: "chain", 2: "truncate", 3: "reference", 4: "general"}
 
 _lib = None

@@ -733,17 +733,19 @@ static void splitk_reduce(xrs_handle_t h, const PTR& P, int count, const double*
         return !(e && e[0] == '0');
     }();
     const size_t MN = size_t(M) * N;
-    KernelTimer timer(h, XRS_KFAM_ELEMWISE, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1));
+    // (its own family: the bench reports the GEMM family's fraction with and without these launches; dispatch
+    // timestamps like the GEMMs')
+    KernelTimer timer(h, XRS_KFAM_SPLITK, count * double(MN) * splits, count * 8.0 * double(MN) * (splits + 1), true);
     if (sym && sym_tiled && N % kSymTile == 0) {
         const unsigned T = unsigned(N / kSymTile);
-        hipLaunchKernelGGL(k_splitk_reduce_sym<PTR>, dim3(T * (T + 1) / 2, unsigned(count)), dim3(256), 0, h->stream, P, slab,
-                           N, splits, alpha);
+        hipExtLaunchKernelGGL(k_splitk_reduce_sym<PTR>, dim3(T * (T + 1) / 2, unsigned(count)), dim3(256), 0, h->stream,
+                              timer.start(), timer.stop(), 0, P, slab, N, splits, alpha);
         check_launch("k_splitk_reduce_sym");
         return;
     }
     const unsigned blocks = unsigned(std::min<size_t>((MN + 255) / 256, 4096));
-    hipLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, P, slab, MN, splits,
-                       alpha, sym ? N : 0);
+    hipExtLaunchKernelGGL(k_splitk_reduce<PTR>, dim3(blocks, unsigned(count)), dim3(256), 0, h->stream, timer.start(),
+                          timer.stop(), 0, P, slab, MN, splits, alpha, sym ? N : 0);
     check_launch("k_splitk_reduce");
 }
 
