@@ -395,8 +395,64 @@ static void svd_big(xrs_handle_t h, const double* A, size_t m, size_t n, double*
     orthogonalize(h, Uq.d(), m, n, false, U, Rn.d());
 }
 
+__global__ void __launch_bounds__(1024) k_amax(const double* __restrict__ x, size_t n, double* __restrict__ out) {
+    __shared__ double red[16];
+    double mx = 0.0;
+    for (size_t e = threadIdx.x; e < n; e += 1024) {
+        const double d = fabs(x[e]);
+        mx = (d > mx || d != d) ? d : mx;   // NaN propagates
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double t = __shfl_xor(mx, o, 64);
+        mx = (t > mx || t != t) ? t : mx;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double v = red[0];
+        for (int i = 1; i < 16; ++i) v = (red[i] > v || red[i] != red[i]) ? red[i] : v;
+        out[0] = v;
+    }
+}
+
+static void svd_core(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt);
+
 void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
+    if (m == n && n >= 16 && n <= 128 && svd_bidiag_mode() != 0) {   // (scale-safe by construction)
+        double diag[4];
+        if (svd_bidiag(h, A, int(n), U, S, Vt, diag)) return;
+        if (svd_bidiag_mode() == 2) {
+            char msg[200];
+            std::snprintf(msg, sizeof msg, "svd_bidiag: check failed (residual %.3g, orthogonality %.3g / %.3g, status %d)", diag[0],
+                          diag[1], diag[2], int(diag[3]));
+            throw Error{XRS_ENUMERIC, msg};
+        }
+    }
+    // range control, dgesdd's dlascl of A into [smlnum, bignum] (here by an exact power of two, to max |A| ~ 1):
+    // the Gram-based preconditioning and the Jacobi dots square the entries (unscaled, 1e150-sized entries
+    // overflowed them)
+    double* am_dev = static_cast<double*>(h->dev_scratch) + 48;
+    hipLaunchKernelGGL(k_amax, dim3(1), dim3(1024), 0, h->stream, A, m * n, am_dev);
+    check_launch("k_amax");
+    double* am_host = static_cast<double*>(h->host_scratch) + 48;
+    XRS_HIP(hipMemcpyAsync(am_host, am_dev, 8, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    const double am = am_host[0];
+    if (am > 0.0 && std::isfinite(am) && (am > 0x1p+200 || am < 0x1p-200)) {
+        const int ex = std::ilogb(am);
+        DevBuf As(h, m * n * 8);
+        XRS_HIP(hipMemcpyAsync(As.d(), A, m * n * 8, hipMemcpyDeviceToDevice, h->stream));
+        scal(h, As.d(), std::ldexp(1.0, -ex), m * n);
+        svd_core(h, As.d(), m, n, U, S, Vt);
+        scal(h, S, std::ldexp(1.0, ex), std::min(m, n));
+        return;
+    }
+    svd_core(h, A, m, n, U, S, Vt);
+}
+
+static void svd_core(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
     if (std::min(m, n) > size_t(kSmallMax)) {
         svd_big(h, A, m, n, U, S, Vt);
         return;

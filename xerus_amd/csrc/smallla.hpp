@@ -74,6 +74,12 @@ bool sym_eig_top_fits(int n, int kk);   // the truncating round's policy (n <= 2
 void sym_eig_top(xrs_handle_t h, const double* A, int lda, int n, int kk, double* lam, double* S, double* Ut, int ldu, int* status_dev);
 // Householder tridiagonalisation (syev.hip's k_sytrd): d (n), e (n - 1) of T = Q^T A Q
 void sym_tridiag(xrs_handle_t h, const double* A, int lda, int n, double* d, double* e);
+// Square SVD (2 <= n <= 128) through the bidiagonal and its Golub-Kahan tridiagonal (syev.hip), certified a
+// posteriori (residual and orthogonality <= 6e-15): false -> the outputs are invalid, recompute. diag
+// (optional, 4): relative residual, max |U^T U - I|, max |Vt Vt^T - I|, multisection status. Synchronises.
+// svd_bidiag_mode: XRS_SVD_BIDIAG (0 off, 1 on with the Jacobi fallback (default), 2 strict: failure throws).
+int svd_bidiag_mode();
+bool svd_bidiag(xrs_handle_t h, const double* A, int n, double* U, double* S, double* Vt, double* diag = nullptr);
 bool jacobi_usv_fits(int p, int q);
 void jacobi_usv(xrs_handle_t h, const double* W, int ldw, bool trans, int p, int q, double* U, int ldu, double* S, double* Vt, int ldvt,
                 int* status_dev, int max_sweeps = 40, bool early = false);

@@ -30,6 +30,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -504,7 +505,7 @@ __global__ void __launch_bounds__(512) k_sytrd_l512(const double* __restrict__ A
 // Zt (kk x ldz): row q = the eigenvector of T (normalised); lam[q]. status[0] <- -1 if a multisection
 // did not reach full precision.
 constexpr int SW_WAVES = 4;   // waves of the multisection (k_stebz_stein)
-template <int NEWTON>
+template <int NEWTON, int ITERS = 3>
 __global__ void __launch_bounds__(64 * SW_WAVES) k_stebz_stein(const double* __restrict__ d, const double* __restrict__ e, int n,
                                                      double* __restrict__ lam, double* __restrict__ Zt, int ldz, int* __restrict__ status,
                                                      unsigned long long* __restrict__ stamps) {
@@ -539,8 +540,9 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_stebz_stein(const double* __r
     // those of T) so that |d - x| and e^2 stay O(1) and 4 levels cannot overflow between rescalings
     const double tsc = ldexp(1.0, -ilogb(fmax(amax, 1e-300)));
     for (int i = lane; i < n; i += 64) {
+        const double es = se[i] * tsc;   // (scaled first: e^2 of an O(1e-200) T underflows)
         sds[i] = sd[i] * tsc;
-        se2s[i] = se2[i] * (tsc * tsc);
+        se2s[i] = es * es;
     }
     __syncthreads();
     STEIN_STAMP(1);
@@ -676,7 +678,7 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_stebz_stein(const double* __r
     }
     __syncthreads();
     STEIN_STAMP(4);
-    for (int it = 0; it < 3; ++it) {
+    for (int it = 0; it < ITERS; ++it) {
         if (tid == 0) {   // dgttrs: forward with the interchanges, then back substitution (running values in
                            // registers, each block's 8 levels of LU operands read ahead of its dependent chain)
             // forward: cur' = a_i cur + b_i with (a, b) = (-f, nxt) (no interchange) or (1, -f nxt) (rows i,
@@ -776,9 +778,16 @@ __global__ void __launch_bounds__(64 * SW_WAVES) k_stebz_stein(const double* __r
 // FMA; the reflectors pass through LDS in chunks of 16384 / n rows, staged by the whole workgroup with
 // coalesced loads. (The first version, 16 lanes per vector and 16 vectors per workgroup, ran a 16-deep
 // FMA chain per reflector on only kk / 16 workgroups: 150 us at n = 256, kk = 128.)
+// (blockIdx.y == 1: the second set V2 / tau2 / Zt2 -- the bidiagonal SVD's left and right vectors in one launch)
 template <int ZE>
 __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, const double* __restrict__ tau, int n, int kk,
-                                               double* __restrict__ Zt, int ldz) {
+                                               double* __restrict__ Zt, int ldz, const double* __restrict__ V2,
+                                               const double* __restrict__ tau2, double* __restrict__ Zt2) {
+    if (blockIdx.y) {
+        V = V2;
+        tau = tau2;
+        Zt = Zt2;
+    }
     constexpr int CHUNK_ELEMS = 16384;
     __shared__ double sv[CHUNK_ELEMS], st[SY_MAX];
     for (int e = threadIdx.x; e < n; e += 256) st[e] = e + 1 < n ? tau[e] : 0.0;
@@ -827,8 +836,11 @@ __global__ void __launch_bounds__(256) k_ormtr(const double* __restrict__ V, con
 // cluster are orthonormalised by two passes of modified Gram-Schmidt (in order of decreasing eigenvalue, as
 // dstein reorthogonalises against the earlier vectors of a cluster). One workgroup; without clusters it only
 // scans the eigenvalues.
+// maxc: clusters larger than this are left alone and *status set to -2 (the bidiagonal SVD's fallback signal: its
+// Jacobi route is cheaper than a long Gram-Schmidt chain); status may be null when maxc >= kk.
 __global__ void __launch_bounds__(256) k_cluster_orth(const double* __restrict__ lam, const double* __restrict__ d,
-                                                      const double* __restrict__ e, int n, int kk, double* __restrict__ Zt, int ldz) {
+                                                      const double* __restrict__ e, int n, int kk, double* __restrict__ Zt, int ldz,
+                                                      int maxc, int* __restrict__ status) {
     __shared__ double red[4];
     __shared__ double tnorm;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -854,6 +866,11 @@ __global__ void __launch_bounds__(256) k_cluster_orth(const double* __restrict__
     while (c0 < kk) {
         int c1 = c0 + 1;
         while (c1 < kk && fabs(lam[c1 - 1] - lam[c1]) <= ortol) ++c1;
+        if (c1 - c0 > maxc) {
+            if (tid == 0) status[0] = -2;
+            c0 = c1;
+            continue;
+        }
         for (int j = c0 + 1; j < c1; ++j) {   // cluster [c0, c1): orthonormalise vector j against c0 .. j-1
             double* zj = Zt + size_t(j) * ldz;
             for (int pass = 0; pass < 2; ++pass) {
@@ -876,6 +893,355 @@ __global__ void __launch_bounds__(256) k_cluster_orth(const double* __restrict__
 __global__ void k_sqrt_lam(const double* __restrict__ lam, int kk, double* __restrict__ S) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < kk) S[i] = sqrt(fmax(lam[i], 0.0));
+}
+
+// ---- dense SVD through a bidiagonal (square n <= 128; svd_bidiag below) ------------------------------
+constexpr int BD_MAX = 128, BD_LDA = BD_MAX + 1;   // LDS row stride 129 doubles: row-wise lanes conflict-free
+
+// dlarfg from alpha and ss = ||x(1:)||^2: beta = -sign(alpha) sqrt(alpha^2 + ss), tau = (beta - alpha) / beta, v = x /
+// (alpha - beta) with v_0 = 1; ss = 0 -> tau = 0, beta = alpha. Formed by every thread from the same operands, so
+// bit-identical across the workgroup (no broadcast needed). k_gebrd_sq scales A to max |A| ~ 1 by a power of two
+// first, so the unscaled sum of squares cannot overflow; squares below 2^-1022 of entries below 2^-511 max |A|
+// are lost, which moves B by less than u ||A||.
+__device__ __forceinline__ void bd_reflector(double alpha, double ss, double& beta, double& tau, double& scal) {
+    if (ss == 0.0) {
+        beta = alpha;
+        tau = 0.0;
+        scal = 0.0;
+        return;
+    }
+    // (the reciprocals by the hardware estimate + 2 Newton steps: ~1 ulp, a 5-deep dependent chain where the IEEE
+    // division's is ~10 -- at ~32 cycles per dependent FP64 operation the reflector is on every column's critical path)
+    beta = -copysign(sqrt(fma(alpha, alpha, ss)), alpha);
+    tau = (beta - alpha) * rcp2(beta);
+    scal = rcp2(alpha - beta);
+}
+
+// Householder bidiagonalisation of a square A (n <= 128, row-major) in ONE workgroup (LAPACK dgebd2, m = n): per
+// column j the left reflector H_j on column j (rows j..n-1), then the right reflector G_j on row j (columns
+// j+1..n-1); A = (H_0 ... H_{n-1}) B (G_0 ... G_{n-2})^T, B upper bidiagonal (d_j, e_j).
+// 512 threads (two waves per SIMD), the matrix register-resident: element (r, c) on the thread with r mod 16 =
+// lane mod 16 and c mod 32 = 4 wave + lane / 16 -- 8 rows x 4 columns per thread. The left product w_c =
+// sum_r v_r a_rc is a sum over a 16-lane DPP row (no LDS, no barrier); the right product w_r = sum_c a_rc v_c
+// sums the wave's four DPP rows (permlane16 / permlane32 swaps) and then the 8 waves through LDS. H_j is formed
+// by the DPP row that holds column j, G_j by every thread from row j's entries and partial squares staged in
+// LDS; the reflector vectors go straight to Vl / Vr, so the registers of finished rows and columns are left as
+// they are (every later product meets them with a zero v or a masked w). Row and column blocks of 16 / 32
+// that lie wholly in the finished part are skipped (wave-uniform branches). Four LDS-only barriers per column.
+// Per column ~9.3k cycles at n = 128 (XRS_STAMPS=bd; 490 us): latency-bound -- one DPP stage of a double sum
+// (two v_mov_b32_dpp + v_add_f64) costs ~90 cycles, the H_j owners' two 16-lane sums ~720, the reflector ~320,
+// and every column runs four such chains back to back. Measured before: A staged in LDS with 8 row groups x 128
+// columns per product, 10k cycles per column (542 us; its __syncthreads also drained the per-column global
+// stores); 1024 threads with 4 x 4 elements each, 10.5k cycles (the reductions, masks and the G_j reflector
+// replicated over 16 waves).
+// Outputs: the Golub-Kahan tridiagonal of B (diagonal tgd = 0 (2n), off-diagonal tge = d_0, e_0, d_1, e_1, ...
+// (2n - 1)), whose top n eigenvalues are B's singular values with eigenvectors (v_0, u_0, v_1, u_1, ...) / sqrt 2;
+// the reflectors in k_ormtr's row format (Vl row j: v with v_j = 1, zeros before; Vr row j: v with v_{j+1} = 1,
+// zeros up to j) and their tau (tl, tr: n - 1 used, the length-1 ones are 0); status[0] = 0 (for k_stebz_stein).
+// A is scaled to max |A| ~ 1 by a power of two first (exact; d and e are scaled back), so the reflectors' sums of
+// squares cannot overflow.
+__global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, int n, double* __restrict__ tgd,
+                                                  double* __restrict__ tge, double* __restrict__ Vl, double* __restrict__ tl,
+                                                  double* __restrict__ Vr, double* __restrict__ tr, int* __restrict__ status,
+                                                  unsigned long long* __restrict__ stamps) {
+#define BD_STAMP(p) \
+    do { if (stamps && threadIdx.x == 0) stamps[p] = __builtin_amdgcn_s_memtime(); } while (0)
+    BD_STAMP(0);
+    __shared__ double vbuf[BD_MAX], xbuf[BD_MAX], wbuf[BD_MAX], sqp[32], red[8];
+    __shared__ double rp[8][BD_MAX];
+    __shared__ double obuf[4][BD_MAX];   // d, e, tau_l, tau_r (stored at the end)
+    __shared__ double stau;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rho = lane & 15, sub = lane >> 4, gam = 4 * wave + sub;
+    if (tid == 0) status[0] = 0;
+    double x[8][4];   // x[i][k] = a(rho + 16 i, gam + 32 k)
+    double am = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int r = rho + 16 * i, c = gam + 32 * k;
+            x[i][k] = (r < n && c < n) ? A[size_t(r) * n + c] : 0.0;
+            am = fmax(am, fabs(x[i][k]));
+        }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmax(am, __shfl_xor(am, o, 64));
+    if (lane == 0) red[wave] = am;
+    for (int i = tid; i < 2 * n; i += 512) tgd[i] = 0.0;
+    lds_barrier();
+    am = red[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) am = fmax(am, red[w]);
+    const int ex = am > 0.0 ? ilogb(am) : 0;
+    const double sdn = ldexp(1.0, -ex), sup = ldexp(1.0, ex);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[i][k] *= sdn;
+    BD_STAMP(1);
+    for (int j = 0; j < n; ++j) {
+        BD_STAMP(4 + 4 * j);
+        const int jk = j >> 5, ji = j >> 4;
+        // ---- H_j: the DPP row holding column j (gam == j mod 32); v straight to Vl row j
+        if (gam == (j & 31)) {
+            double y[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                y[i] = x[i][0];
+#pragma unroll
+                for (int k = 1; k < 4; ++k)
+                    if (jk == k) y[i] = x[i][k];   // (jk uniform: a scalar branch)
+            }
+            double ss = 0.0, al = 0.0;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = rho + 16 * i;
+                ss = (r > j) ? fma(y[i], y[i], ss) : ss;
+                al = (r == j) ? y[i] : al;
+            }
+            ss = sum16(ss);
+            al = sum16(al);
+            double beta, tau, sc;
+            bd_reflector(al, ss, beta, tau, sc);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = rho + 16 * i;
+                const double v = r > j ? y[i] * sc : (r == j ? 1.0 : 0.0);
+                vbuf[r] = v;
+                if (r < n) Vl[size_t(j) * n + r] = v;
+            }
+            if (rho == 0) {
+                obuf[0][j] = beta * sup;
+                obuf[2][j] = tau;
+                stau = tau;
+            }
+        }
+        lds_barrier();
+        BD_STAMP(5 + 4 * j);
+        const double taul = stau;
+        if (taul != 0.0) {   // (uniform)
+            double v[8], w[4];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = (16 * i + 15 >= j) ? vbuf[rho + 16 * i] : 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                double p = 0.0;
+                if (32 * k + 31 > j)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (16 * i + 15 >= j) p = fma(v[i], x[i][k], p);
+                w[k] = p;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (32 * k + 31 > j) w[k] = (gam + 32 * k > j) ? sum16(w[k]) * taul : 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (32 * k + 31 > j)
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (16 * i + 15 >= j) x[i][k] = fma(-v[i], w[k], x[i][k]);
+        }
+        if (j + 1 >= n) break;
+        // ---- G_j: row j's entries and partial squares (columns >= j + 2) into LDS
+        if (rho == (j & 15)) {
+            double yr[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                yr[k] = x[0][k];
+#pragma unroll
+                for (int i = 1; i < 8; ++i)
+                    if (ji == i) yr[k] = x[i][k];   // (ji uniform)
+            }
+            double sp = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int c = gam + 32 * k;
+                xbuf[c] = yr[k];
+                sp = (c >= j + 2) ? fma(yr[k], yr[k], sp) : sp;
+            }
+            sqp[gam] = sp;
+        }
+        lds_barrier();
+        BD_STAMP(6 + 4 * j);
+        double t4[4] = {0.0, 0.0, 0.0, 0.0};   // (four interleaved chains)
+#pragma unroll
+        for (int g = 0; g < 32; g += 4)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) t4[u] += sqp[g + u];
+        double betr, taur, scr;
+        bd_reflector(xbuf[j + 1], (t4[0] + t4[1]) + (t4[2] + t4[3]), betr, taur, scr);
+        double vc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int c = gam + 32 * k;
+            vc[k] = c >= j + 2 ? xbuf[c] * scr : (c == j + 1 ? 1.0 : 0.0);
+        }
+        if (rho == 0) {   // Vr row j (the wave's four DPP rows x 4 columns: 32 threads, all 128 columns)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (gam + 32 * k < n) Vr[size_t(j) * n + gam + 32 * k] = vc[k];
+        }
+        if (tid == 0) {
+            obuf[1][j] = betr * sup;
+            obuf[3][j] = taur;
+        }
+        if (taur != 0.0) {   // (uniform)
+            double q[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                double p = 0.0;
+                if (16 * i + 15 > j)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (32 * k + 31 > j) p = fma(x[i][k], vc[k], p);
+                q[i] = p;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (16 * i + 15 > j) q[i] = addx32(addx16(q[i]));
+            if (sub == 0) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    if (16 * i + 15 > j) rp[wave][rho + 16 * i] = q[i];
+            }
+            lds_barrier();
+            BD_STAMP(7 + 4 * j);
+            if (tid < BD_MAX && tid > j) {
+                double t2[2] = {0.0, 0.0};
+#pragma unroll
+                for (int w = 0; w < 8; w += 2) {
+                    t2[0] += rp[w][tid];
+                    t2[1] += rp[w + 1][tid];
+                }
+                wbuf[tid] = (t2[0] + t2[1]) * taur;
+            } else if (tid < BD_MAX) {
+                wbuf[tid] = 0.0;
+            }
+            lds_barrier();
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (16 * i + 15 > j) {
+                    const double wr = wbuf[rho + 16 * i];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (32 * k + 31 > j) x[i][k] = fma(-wr, vc[k], x[i][k]);
+                }
+        }
+    }
+    if (tid == 0) {
+        obuf[2][n - 1] = 0.0;
+        obuf[3][n - 1] = 0.0;
+        obuf[3][n - 2] = 0.0;
+    }
+    lds_barrier();
+    BD_STAMP(2);
+    for (int i = tid; i < n; i += 512) {
+        tge[2 * i] = obuf[0][i];
+        if (i + 1 < n) tge[2 * i + 1] = obuf[1][i];
+        tl[i] = obuf[2][i];
+        tr[i] = obuf[3][i];
+        Vr[size_t(n - 1) * n + i] = 0.0;
+    }
+    BD_STAMP(3);
+#undef BD_STAMP
+}
+
+// Golub-Kahan eigenvectors -> singular vectors of B: row q of Z (2n) = (v_0, u_0, v_1, u_1, ...); Ub / Vb row q =
+// its u / v half, each normalised (one wave per vector). S[q] = max(lam[q], 0), made non-increasing (the
+// multisection's midpoints of equal singular values may differ in the last bits).
+__global__ void __launch_bounds__(256) k_gk_split(const double* __restrict__ Z, const double* __restrict__ lam, int n,
+                                                  double* __restrict__ Ub, double* __restrict__ Vb, double* __restrict__ S) {
+    const int lane = threadIdx.x & 63, q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        double prev = 1e308;
+        for (int i = 0; i < n; ++i) {
+            const double s = fmin(fmax(lam[i], 0.0), prev);
+            S[i] = s;
+            prev = s;
+        }
+    }
+    if (q >= n) return;
+    const double* z = Z + size_t(q) * 2 * n;
+    double su = 0.0, sv = 0.0;
+    for (int k = lane; k < n; k += 64) {
+        const double v = z[2 * k], u = z[2 * k + 1];
+        su = fma(u, u, su);
+        sv = fma(v, v, sv);
+    }
+    su = sum64(su);
+    sv = sum64(sv);
+    const double iu = su > 0.0 ? 1.0 / sqrt(su) : 0.0, iv = sv > 0.0 ? 1.0 / sqrt(sv) : 0.0;
+    for (int k = lane; k < n; k += 64) {
+        Vb[size_t(q) * n + k] = z[2 * k] * iv;
+        Ub[size_t(q) * n + k] = z[2 * k + 1] * iu;
+    }
+}
+
+// First-order CholeskyQR step on the rows of X (nearly orthonormal): G = X X^T = I + E -> Li = I - Elow with Elow =
+// strict_lower(E) + diag(E) / 2, so that Li X is orthonormal to O(||E||^2) (blockIdx.y: the U / V half)
+__global__ void k_first_order_bd(const double* __restrict__ G, int n, double* __restrict__ Li) {
+    const size_t off = size_t(blockIdx.y) * n * n;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n * n; e += gridDim.x * blockDim.x) {
+        const int i = e / n, k = e % n;
+        const double g = G[off + e];
+        Li[off + e] = i > k ? -g : (i == k ? 1.0 - 0.5 * (g - 1.0) : 0.0);
+    }
+}
+
+__global__ void k_scale_rows_bd(const double* __restrict__ X, const double* __restrict__ S, int n, double* __restrict__ Y) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < n * n; e += gridDim.x * blockDim.x) Y[e] = S[e / n] * X[e];
+}
+
+// out[0] = ||(P - A) s||_F^2, out[1] = ||A s||_F^2 with s = 2^-ilogb(max |A|) (no overflow / underflow at any
+// scale of A), out[2] / out[3] = max |G1 - I| / |G2 - I| (NaN -> inf)
+__global__ void __launch_bounds__(1024) k_svd_check(const double* __restrict__ P, const double* __restrict__ A,
+                                                    const double* __restrict__ G1, const double* __restrict__ G2, int n,
+                                                    double* __restrict__ out) {
+    __shared__ double red[4][16];
+    __shared__ double samax;
+    const int w = threadIdx.x >> 6;
+    double am = 0.0;
+    for (int e = threadIdx.x; e < n * n; e += 1024) am = fmax(am, fabs(A[e]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmax(am, __shfl_xor(am, o, 64));
+    if ((threadIdx.x & 63) == 0) red[0][w] = am;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double v = 0.0;
+        for (int i = 0; i < 16; ++i) v = fmax(v, red[0][i]);
+        samax = v;
+    }
+    __syncthreads();
+    const double s = samax > 0.0 ? ldexp(1.0, -ilogb(samax)) : 1.0;
+    double r2 = 0.0, a2 = 0.0, m1 = 0.0, m2 = 0.0;
+    for (int e = threadIdx.x; e < n * n; e += 1024) {
+        const double d = (P[e] - A[e]) * s, as = A[e] * s, id = (e / n == e % n) ? 1.0 : 0.0;
+        r2 = fma(d, d, r2);
+        a2 = fma(as, as, a2);
+        const double g1 = fabs(G1[e] - id), g2 = fabs(G2[e] - id);
+        m1 = (g1 > m1 || g1 != g1) ? (g1 != g1 ? INFINITY : g1) : m1;
+        m2 = (g2 > m2 || g2 != g2) ? (g2 != g2 ? INFINITY : g2) : m2;
+    }
+    r2 = sum64(r2);
+    a2 = sum64(a2);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        m1 = fmax(m1, __shfl_xor(m1, o, 64));
+        m2 = fmax(m2, __shfl_xor(m2, o, 64));
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        red[0][w] = r2;
+        red[1][w] = a2;
+        red[2][w] = m1;
+        red[3][w] = m2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double v = 0.0;
+        for (int i = 0; i < 16; ++i) v = threadIdx.x < 2 ? v + red[threadIdx.x][i] : fmax(v, red[threadIdx.x][i]);
+        out[threadIdx.x] = (v != v) ? INFINITY : v;
+    }
 }
 
 }  // namespace
@@ -927,13 +1293,13 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
     hipLaunchKernelGGL(k_stebz_stein<2>, dim3(kk), dim3(64 * SW_WAVES), 0, h->stream, dbuf.d(), ebuf.d(), n, lm, Ut, ldu, status,
                        stp ? stp + 768 : nullptr);
     check_launch("k_stebz_stein");
-    hipLaunchKernelGGL(k_cluster_orth, dim3(1), dim3(256), 0, h->stream, lm, dbuf.d(), ebuf.d(), n, kk, Ut, ldu);
+    hipLaunchKernelGGL(k_cluster_orth, dim3(1), dim3(256), 0, h->stream, lm, dbuf.d(), ebuf.d(), n, kk, Ut, ldu, kk, nullptr);
     check_launch("k_cluster_orth");
     // (a blocked form -- 16 reflectors' dots together, their recurrence through the block's reflector Gram --
     // measured slower: 162 vs 108 us at order 256, 55 vs 38 us at 128, plus 22-28 us for the Grams; r04ah)
-    if (n <= 64) hipLaunchKernelGGL((k_ormtr<1>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
-    else if (n <= 128) hipLaunchKernelGGL((k_ormtr<2>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
-    else hipLaunchKernelGGL((k_ormtr<4>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu);
+    if (n <= 64) hipLaunchKernelGGL((k_ormtr<1>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu, V.d(), tbuf.d(), Ut);
+    else if (n <= 128) hipLaunchKernelGGL((k_ormtr<2>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu, V.d(), tbuf.d(), Ut);
+    else hipLaunchKernelGGL((k_ormtr<4>), dim3((kk + 3) / 4), dim3(256), 0, h->stream, V.d(), tbuf.d(), n, kk, Ut, ldu, V.d(), tbuf.d(), Ut);
     check_launch("k_ormtr");
     if (stp && n > 64) {   // k_sytrd_l512 column-step phases (cycles, mean over the first 63 steps)
         std::vector<unsigned long long> hl(1024);
@@ -985,6 +1351,114 @@ XRS_REQUIRE(n >= 2 && n <= SY_MAX && kk >= 1 && kk <= n, "sym_eig_top: need 2 <=
         hipLaunchKernelGGL(k_sqrt_lam, dim3((kk + 255) / 256), dim3(256), 0, h->stream, lm, kk, S);
         check_launch("k_sqrt_lam");
     }
+}
+
+// Square SVD (dgesdd's role, n <= 128) without Jacobi sweeps: B = bidiagonal of A (k_gebrd_sq), its singular
+// triplets as the top n eigenpairs of the Golub-Kahan tridiagonal of order 2n (the multisection + inverse
+// iteration of sym_eig_top; clusters up to 24 vectors orthonormalised), the u / v halves back-transformed by the
+// reflectors (k_ormtr, both sets in one launch) and re-orthonormalised by one first-order CholeskyQR step on their
+// rows (inverse iteration leaves each half's error toward the -sigma partners at u ||A|| / sigma, so the
+// correction changes U S Vt by O(u ||A||)). The result is certified a posteriori: ||U S Vt - A||_F <= 6e-15
+// ||A||_F and max |U^T U - I|, |Vt Vt^T - I| <= 6e-15 (dgesdd measured 1e-15..3e-15 on these shapes) -- else
+// false and the caller recomputes with Jacobi: spectra with clusters beyond 24 (graded over many decades, flat,
+// rank-deficient), whose vectors inverse iteration cannot separate cheaply. Synchronises (the check).
+// n = 128 (profiles/r06/svd_bidiag_*): 0.84 ms against 1.6 ms of Jacobi; k_gebrd_sq 490 us of it, k_stebz_stein
+// 150 us, the rest 30-40 us launches.
+int svd_bidiag_mode() {
+    static const int mode = std::getenv("XRS_SVD_BIDIAG") ? std::atoi(std::getenv("XRS_SVD_BIDIAG")) : 1;
+    return mode;
+}
+
+bool svd_bidiag(xrs_handle_t h, const double* A, int n, double* U, double* S, double* Vt, double* diag) {
+    XRS_REQUIRE(n >= 2 && n <= BD_MAX, "svd_bidiag: need 2 <= n <= 128");
+    const size_t nn = size_t(n) * n;
+    // (Ub, Vb adjacent: the halves' first-order steps run as one batch; W holds the Grams, then Li)
+    DevBuf tg(h, size_t(4 * n) * 8), Vl(h, nn * 8), Vr(h, nn * 8), taus(h, size_t(2 * n) * 8), lam(h, size_t(n) * 8),
+        Z(h, nn * 2 * 8), UVb(h, nn * 2 * 8), W(h, nn * 2 * 8), Ut(h, nn * 8), st(h, 64), chk(h, 64);
+    double *tgd = tg.d(), *tge = tg.d() + 2 * n, *tl = taus.d(), *tr = taus.d() + n, *Ub = UVb.d(), *Vb = UVb.d() + nn;
+    {
+        KernelTimer timer(h, XRS_KFAM_SVD, 8.0 / 3.0 * double(nn) * n + 8.0 * double(nn) * n, 8.0 * double(nn) * 4);
+        static const bool want_stamps = stamps_enabled("bd");
+        DevBuf sb(h, want_stamps ? 1024 * 8 : 0);
+        unsigned long long* stp = want_stamps ? sb.as<unsigned long long>() : nullptr;
+        if (stp) XRS_HIP(hipMemsetAsync(stp, 0, 1024 * 8, h->stream));
+        hipLaunchKernelGGL(k_gebrd_sq, dim3(1), dim3(512), 0, h->stream, A, n, tgd, tge, Vl.d(), tl, Vr.d(), tr, st.as<int>(), stp);
+        check_launch("k_gebrd_sq");
+        if (stp) {   // k_gebrd_sq phases (cycles): prologue, per column (H partial, H update + squares, G phase), epilogue
+            std::vector<unsigned long long> hs(1024);
+            XRS_HIP(hipMemcpyAsync(hs.data(), stp, 1024 * 8, hipMemcpyDeviceToHost, h->stream));
+            XRS_HIP(hipStreamSynchronize(h->stream));
+            double ph[3] = {0, 0, 0};
+            int steps = 0;
+            for (int j = 0; j + 1 < n - 1; ++j) {
+                const unsigned long long* q = hs.data() + 4 + 4 * j;
+                if (!q[0] || !q[1] || !q[2] || !q[4]) continue;
+                ph[0] += double(q[1] - q[0]);
+                ph[1] += double(q[2] - q[1]);
+                ph[2] += double(q[4] - q[2]);
+                ++steps;
+            }
+            std::fprintf(stderr, "k_gebrd_sq n=%d: total %llu prologue %llu epilogue %llu; mean per column over %d: H_j %.0f left product + row j %.0f G_j %.0f; "
+                         "column 0: %llu %llu %llu\n", n, hs[3] - hs[0], hs[1] - hs[0], hs[3] - hs[2], steps, ph[0] / steps, ph[1] / steps,
+                         ph[2] / steps, hs[5] - hs[4], hs[6] - hs[5], hs[8] - hs[6]);
+        }
+        static const int iters = std::getenv("XRS_BD_ITERS") ? std::atoi(std::getenv("XRS_BD_ITERS")) : 3;
+        if (iters == 2)
+            hipLaunchKernelGGL((k_stebz_stein<2, 2>), dim3(n), dim3(64 * SW_WAVES), 0, h->stream, tgd, tge, 2 * n, lam.d(), Z.d(),
+                               2 * n, st.as<int>(), nullptr);
+        else
+            hipLaunchKernelGGL((k_stebz_stein<2, 3>), dim3(n), dim3(64 * SW_WAVES), 0, h->stream, tgd, tge, 2 * n, lam.d(), Z.d(),
+                               2 * n, st.as<int>(), nullptr);
+        check_launch("k_stebz_stein");
+        hipLaunchKernelGGL(k_cluster_orth, dim3(1), dim3(256), 0, h->stream, lam.d(), tgd, tge, 2 * n, n, Z.d(), 2 * n, 24,
+                           st.as<int>());
+        check_launch("k_cluster_orth");
+        hipLaunchKernelGGL(k_gk_split, dim3((n + 3) / 4), dim3(256), 0, h->stream, Z.d(), lam.d(), n, Ub, Vb, S);
+        check_launch("k_gk_split");
+        if (n <= 64)
+            hipLaunchKernelGGL((k_ormtr<1>), dim3((n + 3) / 4, 2), dim3(256), 0, h->stream, Vl.d(), tl, n, n, Ub, n, Vr.d(), tr, Vb);
+        else
+            hipLaunchKernelGGL((k_ormtr<2>), dim3((n + 3) / 4, 2), dim3(256), 0, h->stream, Vl.d(), tl, n, n, Ub, n, Vr.d(), tr, Vb);
+        check_launch("k_ormtr");
+    }
+    // the halves' rows orthonormalised by one first-order CholeskyQR step (their Grams are I + O(u ||T|| / gap)
+    // outside the clusters; a half that needs more fails the check below)
+    {
+        double* Gp[2] = {W.d(), W.d() + nn};
+        const double* Xp[2] = {Ub, Vb};
+        gemm_batched(h, 2, Gp, size_t(n), size_t(n), 1.0, Xp, size_t(n), false, size_t(n), Xp, size_t(n), true, true);
+        hipLaunchKernelGGL(k_first_order_bd, dim3((unsigned(nn) + 255) / 256, 2), dim3(256), 0, h->stream, W.d(), n, W.d());
+        check_launch("k_first_order_bd");
+        double* Qp[2] = {Ut.d(), Vt};
+        const double* Lp[2] = {W.d(), W.d() + nn};
+        gemm_batched(h, 2, Qp, size_t(n), size_t(n), 1.0, Lp, size_t(n), false, size_t(n), Xp, size_t(n), false, false, kTriA);
+    }
+    transpose(h, U, Ut.d(), size_t(n), size_t(n));
+    // a posteriori check (Ub / Vb / W / Z reused as scratch)
+    hipLaunchKernelGGL(k_scale_rows_bd, dim3((nn + 255) / 256), dim3(256), 0, h->stream, Vt, S, n, Ub);
+    check_launch("k_scale_rows_bd");
+    gemm(h, Vb, size_t(n), size_t(n), 1.0, U, size_t(n), false, size_t(n), Ub, size_t(n), false);   // U S Vt
+    {
+        double* Gp[2] = {Z.d(), Z.d() + nn};
+        const double* Xp[2] = {Ut.d(), Vt};
+        gemm_batched(h, 2, Gp, size_t(n), size_t(n), 1.0, Xp, size_t(n), false, size_t(n), Xp, size_t(n), true, true);   // U^T U, Vt Vt^T
+    }
+    hipLaunchKernelGGL(k_svd_check, dim3(1), dim3(1024), 0, h->stream, Vb, A, Z.d(), Z.d() + nn, n, chk.d());
+    check_launch("k_svd_check");
+    double* hc = static_cast<double*>(h->host_scratch) + 80;   // (pinned; a slot of its own)
+    XRS_HIP(hipMemcpyAsync(hc, chk.d(), 32, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipMemcpyAsync(hc + 4, st.d(), 4, hipMemcpyDeviceToHost, h->stream));
+    XRS_HIP(hipStreamSynchronize(h->stream));
+    int hs = 0;
+    std::memcpy(&hs, hc + 4, 4);
+    const double res = std::sqrt(hc[0]), anorm = std::sqrt(hc[1]);
+    if (diag) {
+        diag[0] = anorm > 0.0 ? res / anorm : res;
+        diag[1] = hc[2];
+        diag[2] = hc[3];
+        diag[3] = hs;
+    }
+    return hs == 0 && res <= 6e-15 * anorm && hc[2] <= 6e-15 && hc[3] <= 6e-15;
 }
 
 }  // namespace xrs
