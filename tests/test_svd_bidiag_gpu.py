@@ -33,10 +33,13 @@ def spectra():
     V, _ = np.linalg.qr(rng.standard_normal((n, n)))
     yield "graded", (U * np.logspace(0, -1, n)) @ V.T   # (gaps above dstein's cluster tolerance 1e-3 ||T||)
     yield "tiny", rng.standard_normal((n, n)) * 1e-200
+    for m, q in ((128, 1500), (1500, 128), (64, 700), (300, 100), (24, 400)):   # (the QR factor's route)
+        yield "g%%dx%%d" %% (m, q), rng.standard_normal((m, q))
 for name, A in spectra():
     Uh, Sh, Vh = (x.numpy() for x in h.svd(h.array(A)))
     Sr = ref.svd(A)[1]
     k = Sh.size
+    assert Uh.shape == (A.shape[0], k) and Vh.shape == (k, A.shape[1])
     sc = 1.0 / np.abs(A).max()
     out.append(dict(name=name, res=float(np.linalg.norm(((Uh * Sh) @ Vh - A) * sc) / np.linalg.norm(A * sc)),
                     ou=float(np.abs(Uh.T @ Uh - np.eye(k)).max()), ov=float(np.abs(Vh @ Vh.T - np.eye(k)).max()),

@@ -26,6 +26,8 @@ def cases(rng):
     yield "rank100", rng.standard_normal((n, 100)) @ rng.standard_normal((100, n))
     yield "scaled1e150", rng.standard_normal((n, n)) * 1e150
     yield "scaled1e-200", rng.standard_normal((n, n)) * 1e-200
+    for m, k in ((128, 2560), (2560, 128), (64, 1000), (300, 100), (48, 500), (32, 500)):
+        yield f"g{m}x{k}", rng.standard_normal((m, k))
 
 
 def main():
@@ -47,7 +49,7 @@ def main():
         k = Sh.size
         sc = 1.0 / np.abs(A).max()
         res = np.linalg.norm(((Uh * Sh) @ Vh - A) * sc) / np.linalg.norm(A * sc)
-        ou = np.abs(Uh.T @ Uh - np.eye(k)).max()
+        ou = np.abs(Uh.T @ Uh - np.eye(k)).max()   # (k = min(m, n))
         ov = np.abs(Vh @ Vh.T - np.eye(k)).max()
         se = np.abs(Sh - Sr).max() / Sr[0]
         h.synchronize()

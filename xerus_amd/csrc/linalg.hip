@@ -418,18 +418,24 @@ __global__ void __launch_bounds__(1024) k_amax(const double* __restrict__ x, siz
 
 static void svd_core(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt);
 
+// the bidiagonal route (syev.hip svd_bidiag) on a square n x n A; false: run the Jacobi route (XRS_SVD_BIDIAG=2:
+// a failed check throws instead)
+static bool try_bidiag(xrs_handle_t h, const double* A, size_t n, double* U, double* S, double* Vt) {
+    double diag[4];
+    if (svd_bidiag(h, A, int(n), U, S, Vt, diag)) return true;
+    if (svd_bidiag_mode() == 2) {
+        char msg[200];
+        std::snprintf(msg, sizeof msg, "svd_bidiag: check failed (residual %.3g, orthogonality %.3g / %.3g, status %d)", diag[0],
+                      diag[1], diag[2], int(diag[3]));
+        throw Error{XRS_ENUMERIC, msg};
+    }
+    return false;
+}
+
 void svd(xrs_handle_t h, const double* A, size_t m, size_t n, double* U, double* S, double* Vt) {
     XRS_REQUIRE(m > 0 && n > 0, "Dimension m and n must be larger than zero");
-    if (m == n && n >= 16 && n <= 128 && svd_bidiag_mode() != 0) {   // (scale-safe by construction)
-        double diag[4];
-        if (svd_bidiag(h, A, int(n), U, S, Vt, diag)) return;
-        if (svd_bidiag_mode() == 2) {
-            char msg[200];
-            std::snprintf(msg, sizeof msg, "svd_bidiag: check failed (residual %.3g, orthogonality %.3g / %.3g, status %d)", diag[0],
-                          diag[1], diag[2], int(diag[3]));
-            throw Error{XRS_ENUMERIC, msg};
-        }
-    }
+    // square 16..128: the bidiagonal route on A itself (scale-safe by construction)
+    if (m == n && n >= 16 && n <= 128 && svd_bidiag_mode() != 0 && try_bidiag(h, A, n, U, S, Vt)) return;
     // range control, dgesdd's dlascl of A into [smlnum, bignum] (here by an exact power of two, to max |A| ~ 1):
     // the Gram-based preconditioning and the Jacobi dots square the entries (unscaled, 1e150-sized entries
     // overflowed them)
@@ -457,21 +463,24 @@ static void svd_core(xrs_handle_t h, const double* A, size_t m, size_t n, double
         svd_big(h, A, m, n, U, S, Vt);
         return;
     }
-    if (m <= n && jacobi_usv_fits(int(m), int(n))) {
+    const size_t k = std::min(m, n);
+    // non-square with 24 <= min(m, n) <= 128: the bidiagonal route on the QR factor (profiles/r06/svd_bidiag_*:
+    // 64 x 1000 0.61 vs 5.1 ms, 128 x 2560 1.11 vs 1.71 ms, 300 x 100 0.80 vs 1.45 ms against Jacobi)
+    const bool bd = m != n && k >= 24 && k <= 128 && svd_bidiag_mode() != 0;
+    if (!bd && m <= n && jacobi_usv_fits(int(m), int(n))) {
         jacobi_svd_rows(h, A, int(m), int(n), U, S, Vt);   // rows of A directly
         return;
     }
     // preconditioned (the QR factor's rows are shorter and better conditioned for Jacobi):
     //   wide A = R Q: R = U S Vr, Vt = Vr Q;   tall A = Q R: R = U_R S Vt, U = Q U_R
-    const size_t k = std::min(m, n);
     DevBuf R(h, k * k * 8), Qf(h, m * n * 8), F(h, k * k * 8);
     if (m <= n) {
         rq(h, A, m, n, R.d(), Qf.d());
-        jacobi_svd_rows(h, R.d(), int(k), int(k), U, S, F.d());
+        if (!(bd && try_bidiag(h, R.d(), k, U, S, F.d()))) jacobi_svd_rows(h, R.d(), int(k), int(k), U, S, F.d());
         gemm(h, Vt, k, n, 1.0, F.d(), k, false, k, Qf.d(), n, false);
     } else {
         qr(h, A, m, n, Qf.d(), R.d());
-        jacobi_svd_rows(h, R.d(), int(k), int(k), F.d(), S, Vt);
+        if (!(bd && try_bidiag(h, R.d(), k, F.d(), S, Vt))) jacobi_svd_rows(h, R.d(), int(k), int(k), F.d(), S, Vt);
         gemm(h, U, m, k, 1.0, Qf.d(), k, false, k, F.d(), k, false);
     }
 }
