@@ -76,10 +76,12 @@ def main():
     e_ref, _ = tt_diff_norm(og.cores, xg.cores)
     out["graded_ranks_ok"] = gg.ranks == og.ranks
     out["graded_err_diff"] = abs(e_gpu - e_ref) / nrm
-    # flat spectra cut inside the cluster (the Jacobi early stop on repeated singular values): x has
-    # cores that are left- AND right-orthonormal, so every edge's singular values are all 1; x + x is rank
-    # deficient (general path) with edge spectra {2 (r times), 0}; round(r / 2) cuts inside the cluster. The kept
-    # subspace is not unique there, the ranks and the truncation error are
+    # flat spectra cut inside the cluster (repeated singular values): x has cores that are left- AND
+    # right-orthonormal, so every edge's singular values are all 1; x + x has edge spectra {2 (r times), 0} and its
+    # left end is structurally rank deficient (the exact QC steps; on the GPU it ends on the reference's sweep);
+    # round(r / 2) cuts inside the cluster. The kept subspace of the first cut is arbitrary within the cluster and
+    # the later edges' spectra depend on it, so only the ranks and the TT-SVD quasi-optimality (each error within
+    # sqrt(d - 1) of the other's) are comparable with the oracle -- not the error itself
     fr, fn, fd = 10, 10, 6
     frng = np.random.default_rng(11)
     fc = [np.linalg.qr(frng.standard_normal((fn, fr)))[0].reshape(1, fn, fr)]
@@ -95,11 +97,18 @@ def main():
     e_gpu, nrm = tt_diff_norm(gf.cores(), xs.cores)
     e_ref, _ = tt_diff_norm(of.cores, xs.cores)
     out["flat_ranks_ok"] = gf.ranks == of.ranks
-    out["flat_err_diff"] = abs(e_gpu - e_ref) / nrm
+    out["flat_err_gpu"], out["flat_err_ref"] = e_gpu / nrm, e_ref / nrm
+    q = np.sqrt(fd - 1.0) * (1.0 + 1e-8)
+    out["flat_err_ok"] = bool(e_gpu <= q * e_ref and e_ref <= q * e_gpu)
     # the block Jacobi right singular vectors (xrs_svd_rows_vt) and the eigensolver entry (xrs_sym_eig_top)
     W = rng.standard_normal((64, 96))
     S, Vt, sweeps = h.svd_rows_vt(h.array(W))
     out["svd_err"] = float(np.abs(S.numpy() - np.linalg.svd(W, compute_uv=False)).max() / np.linalg.norm(W, 2))
+    # the dense API SVD (square: the bidiagonal route unless XRS_SVD_BIDIAG=0)
+    Ad = rng.standard_normal((96, 96))
+    Ua, Sa, Va = (x.numpy() for x in h.svd(h.array(Ad)))
+    out["api_svd_res"] = float(np.linalg.norm((Ua * Sa) @ Va - Ad) / np.linalg.norm(Ad))
+    out["api_svd_orth"] = float(max(np.abs(Ua.T @ Ua - np.eye(96)).max(), np.abs(Va @ Va.T - np.eye(96)).max()))
     P = W @ W.T
     lam, Ut, st = h.sym_eig_top(h.array(P), 8)
     out["eig_err"] = float(np.abs(lam.numpy() - np.linalg.eigvalsh(P)[::-1][:8]).max() / np.linalg.norm(P, 2))
