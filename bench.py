@@ -674,8 +674,10 @@ def main():
                 if prof["ms"] > 0 else 0.0,
                 "reduce_launches_per_step": prof_red["launches"] / args.steps,
                 "reduce_us_per_launch": round(prof_red["ms"] / max(1, prof_red["launches"]) * 1e3, 3),
+                "traffic": traffic.get("hbm_bytes_per_launch_incl_splitk_reduce") if traffic else None,
                 "note": "the GEMM family's flops over the GEMM launches' AND the separate split-K reduce launches' summed "
-                        "durations (same sequential steps, reduce launches timed in a pass of their own)",
+                        "durations (same sequential steps, reduce launches timed in a pass of their own); traffic: the GEMM "
+                        "launches' HBM bytes plus the reduce launches' spread over them (same PMC passes)",
             },
             "algorithmic_flops_per_launch": prof["flops"] / launches,
             "algorithmic_bytes_per_launch": prof["bytes"] / launches,

@@ -74,6 +74,24 @@ if "FETCH_SIZE" in g and "WRITE_SIZE" in g:
                   ", mean per GEMM dispatch (k_gemm_glds + k_gemm_f64), corrected by the 8-B load/store calibration of "
                   "tools/fetch_calib.hip (FETCH x%.3f, WRITE x%.3f); %s/pmc_summary.json" % (ff, wf, dst),
     }
+    # the separate split-K reduce launches (k_splitk_reduce, k_splitk_reduce_sym) of the same passes: their bytes
+    # summed and spread over the GEMM dispatches (the GEMM family's traffic with its reduce launches included)
+    red = {"FETCH_SIZE": 0.0, "WRITE_SIZE": 0.0}
+    nred = 0
+    for p_ in ("fetch", "write"):
+        for fam, counters in load(p_).items():
+            if not fam.startswith("xrs::k_splitk_reduce"):
+                continue
+            for c, v in counters.items():
+                if c in red:
+                    red[c] += sum(v)
+                    if c == "FETCH_SIZE":
+                        nred += len(v)
+    if nred:
+        rb = red["FETCH_SIZE"] * 1024 * ff + red["WRITE_SIZE"] * 1024 * wf
+        out["splitk_reduce"] = {"dispatches": nred, "hbm_bytes_per_reduce": rb / nred,
+                                "hbm_bytes_per_gemm_launch": rb / g["FETCH_SIZE"]["dispatches"]}
+        out["hbm_bytes_per_launch_incl_splitk_reduce"] = fetch + write + rb / g["FETCH_SIZE"]["dispatches"]
     if "SQ_VALU_MFMA_BUSY_CYCLES" in g and "GRBM_GUI_ACTIVE" in g:
         out["mfma_busy_cycles_per_dispatch"] = g["SQ_VALU_MFMA_BUSY_CYCLES"]["mean"]
         out["gui_active_cycles_per_dispatch"] = g["GRBM_GUI_ACTIVE"]["mean"]
