@@ -1005,9 +1005,8 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
                 const int r = rho + 16 * i;
-                const double v = r > j ? y[i] * sc : (r == j ? 1.0 : 0.0);
-                vbuf[r] = v;
-                if (r < n) Vl[size_t(j) * n + r] = v;
+                y[i] = r > j ? y[i] * sc : (r == j ? 1.0 : 0.0);
+                vbuf[r] = y[i];
             }
             if (rho == 0) {
                 obuf[0][j] = beta * sup;
@@ -1016,6 +1015,13 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
             }
         }
         lds_barrier();
+        if (gam == (j & 31)) {   // Vl row j, after the barrier (off the other waves' wait)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = rho + 16 * i;
+                if (r < n) Vl[size_t(j) * n + r] = vbuf[r];
+            }
+        }
         BD_STAMP(5 + 4 * j);
         const double taul = stau;
         if (taul != 0.0) {   // (uniform)
@@ -1070,16 +1076,12 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
             for (int u = 0; u < 4; ++u) t4[u] += sqp[g + u];
         double betr, taur, scr;
         bd_reflector(xbuf[j + 1], (t4[0] + t4[1]) + (t4[2] + t4[3]), betr, taur, scr);
+        if (stamps && tid == 0 && j < 96) stamps[600 + 4 * j] = __builtin_amdgcn_s_memtime() + (unsigned long long)(scr * 0.0);
         double vc[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int c = gam + 32 * k;
             vc[k] = c >= j + 2 ? xbuf[c] * scr : (c == j + 1 ? 1.0 : 0.0);
-        }
-        if (rho == 0) {   // Vr row j (the wave's four DPP rows x 4 columns: 32 threads, all 128 columns)
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (gam + 32 * k < n) Vr[size_t(j) * n + gam + 32 * k] = vc[k];
         }
         if (tid == 0) {
             obuf[1][j] = betr * sup;
@@ -1104,8 +1106,14 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
                 for (int i = 0; i < 8; ++i)
                     if (16 * i + 15 > j) rp[wave][rho + 16 * i] = q[i];
             }
+            if (stamps && tid == 0 && j < 96) stamps[601 + 4 * j] = __builtin_amdgcn_s_memtime();
             lds_barrier();
             BD_STAMP(7 + 4 * j);
+            if (rho == 0) {   // Vr row j (the wave's four DPP rows x 4 columns: 32 threads, all 128 columns)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (gam + 32 * k < n) Vr[size_t(j) * n + gam + 32 * k] = vc[k];
+            }
             if (tid < BD_MAX && tid > j) {
                 double t2[2] = {0.0, 0.0};
 #pragma unroll
@@ -1118,6 +1126,7 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
                 wbuf[tid] = 0.0;
             }
             lds_barrier();
+            if (stamps && tid == 0 && j < 96) stamps[602 + 4 * j] = __builtin_amdgcn_s_memtime();
 #pragma unroll
             for (int i = 0; i < 8; ++i)
                 if (16 * i + 15 > j) {
@@ -1126,6 +1135,10 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
                     for (int k = 0; k < 4; ++k)
                         if (32 * k + 31 > j) x[i][k] = fma(-wr, vc[k], x[i][k]);
                 }
+        } else if (rho == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (gam + 32 * k < n) Vr[size_t(j) * n + gam + 32 * k] = vc[k];
         }
     }
     if (tid == 0) {
@@ -1397,6 +1410,23 @@ bool svd_bidiag(xrs_handle_t h, const double* A, int n, double* U, double* S, do
                 ph[1] += double(q[2] - q[1]);
                 ph[2] += double(q[4] - q[2]);
                 ++steps;
+            }
+            {
+                double gp[5] = {0, 0, 0, 0, 0};
+                int cnt = 0;
+                for (int j = 0; j < std::min(n - 2, 95); ++j) {
+                    const unsigned long long* q = hs.data() + 600 + 4 * j;
+                    const unsigned long long g0 = hs[6 + 4 * j], b3 = hs[7 + 4 * j], nx = hs[8 + 4 * j];
+                    if (!q[0] || !q[1] || !q[2] || !g0 || !b3 || !nx) continue;
+                    gp[0] += double(q[0] - g0);   // ss + reflector
+                    gp[1] += double(q[1] - q[0]);   // vc, right product, partials
+                    gp[2] += double(b3 - q[1]);     // barrier 3
+                    gp[3] += double(q[2] - b3);     // wsum + barrier 4
+                    gp[4] += double(nx - q[2]);     // right update
+                    ++cnt;
+                }
+                std::fprintf(stderr, "k_gebrd_sq n=%d G_j thread 0: reflector %.0f right product %.0f barrier3 %.0f wsum+barrier4 %.0f update %.0f (over %d)\n",
+                             n, gp[0] / cnt, gp[1] / cnt, gp[2] / cnt, gp[3] / cnt, gp[4] / cnt, cnt);
             }
             std::fprintf(stderr, "k_gebrd_sq n=%d: total %llu prologue %llu epilogue %llu; mean per column over %d: H_j %.0f left product + row j %.0f G_j %.0f; "
                          "column 0: %llu %llu %llu\n", n, hs[3] - hs[0], hs[1] - hs[0], hs[3] - hs[2], steps, ph[0] / steps, ph[1] / steps,
