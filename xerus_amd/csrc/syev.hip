@@ -948,7 +948,8 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
     do { if (stamps && threadIdx.x == 0) stamps[p] = __builtin_amdgcn_s_memtime(); } while (0)
     BD_STAMP(0);
     __shared__ double vbuf[BD_MAX], xbuf[BD_MAX], wbuf[BD_MAX], sqp[32], red[8];
-    __shared__ double rp[8][BD_MAX];
+    __shared__ double rp[32][BD_MAX + 16];   // right-product partials per column residue (row stride: sub
+                                             // offsets land 32 banks apart -- conflict-free half waves)
     __shared__ double obuf[4][BD_MAX];   // d, e, tau_l, tau_r (stored at the end)
     __shared__ double stau;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, rho = lane & 15, sub = lane >> 4, gam = 4 * wave + sub;
@@ -984,13 +985,14 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
         // ---- H_j: the DPP row holding column j (gam == j mod 32); v straight to Vl row j
         if (gam == (j & 31)) {
             double y[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                y[i] = x[i][0];
-#pragma unroll
-                for (int k = 1; k < 4; ++k)
-                    if (jk == k) y[i] = x[i][k];   // (jk uniform: a scalar branch)
+#define BD_COL(K) for (int i = 0; i < 8; ++i) y[i] = x[i][K]
+            switch (jk) {   // (uniform: a scalar branch, not selects over all 32 registers)
+                case 0: BD_COL(0); break;
+                case 1: BD_COL(1); break;
+                case 2: BD_COL(2); break;
+                default: BD_COL(3); break;
             }
+#undef BD_COL
             double ss = 0.0, al = 0.0;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
@@ -1051,13 +1053,18 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
         // ---- G_j: row j's entries and partial squares (columns >= j + 2) into LDS
         if (rho == (j & 15)) {
             double yr[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                yr[k] = x[0][k];
-#pragma unroll
-                for (int i = 1; i < 8; ++i)
-                    if (ji == i) yr[k] = x[i][k];   // (ji uniform)
+#define BD_ROW(I) for (int k = 0; k < 4; ++k) yr[k] = x[I][k]
+            switch (ji) {   // (uniform)
+                case 0: BD_ROW(0); break;
+                case 1: BD_ROW(1); break;
+                case 2: BD_ROW(2); break;
+                case 3: BD_ROW(3); break;
+                case 4: BD_ROW(4); break;
+                case 5: BD_ROW(5); break;
+                case 6: BD_ROW(6); break;
+                default: BD_ROW(7); break;
             }
+#undef BD_ROW
             double sp = 0.0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -1098,14 +1105,11 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
                         if (32 * k + 31 > j) p = fma(x[i][k], vc[k], p);
                 q[i] = p;
             }
+            // (every lane's partials to LDS: 32 per row, summed below -- the permlane16 / permlane32 sums of the
+            // wave's four DPP rows first cost ~2k cycles per column, their dependent chains on the critical path)
 #pragma unroll
             for (int i = 0; i < 8; ++i)
-                if (16 * i + 15 > j) q[i] = addx32(addx16(q[i]));
-            if (sub == 0) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    if (16 * i + 15 > j) rp[wave][rho + 16 * i] = q[i];
-            }
+                if (16 * i + 15 > j) rp[gam][rho + 16 * i] = q[i];
             if (stamps && tid == 0 && j < 96) stamps[601 + 4 * j] = __builtin_amdgcn_s_memtime();
             lds_barrier();
             BD_STAMP(7 + 4 * j);
@@ -1115,13 +1119,12 @@ __global__ void __launch_bounds__(512) k_gebrd_sq(const double* __restrict__ A, 
                     if (gam + 32 * k < n) Vr[size_t(j) * n + gam + 32 * k] = vc[k];
             }
             if (tid < BD_MAX && tid > j) {
-                double t2[2] = {0.0, 0.0};
+                double t4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                for (int w = 0; w < 8; w += 2) {
-                    t2[0] += rp[w][tid];
-                    t2[1] += rp[w + 1][tid];
-                }
-                wbuf[tid] = (t2[0] + t2[1]) * taur;
+                for (int g = 0; g < 32; g += 4)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) t4[u] += rp[g + u][tid];
+                wbuf[tid] = ((t4[0] + t4[1]) + (t4[2] + t4[3])) * taur;
             } else if (tid < BD_MAX) {
                 wbuf[tid] = 0.0;
             }
