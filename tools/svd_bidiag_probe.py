@@ -26,6 +26,11 @@ def cases(rng):
     yield "rank100", rng.standard_normal((n, 100)) @ rng.standard_normal((100, n))
     yield "scaled1e150", rng.standard_normal((n, n)) * 1e150
     yield "scaled1e-200", rng.standard_normal((n, n)) * 1e-200
+    for m in (256, 512):
+        yield f"gauss{m}", rng.standard_normal((m, m))
+        U, _ = np.linalg.qr(rng.standard_normal((m, m)))
+        V, _ = np.linalg.qr(rng.standard_normal((m, m)))
+        yield f"graded{m}", (U * np.logspace(0, -12, m)) @ V.T
     for m, k in ((128, 2560), (2560, 128), (64, 1000), (300, 100), (48, 500), (32, 500)):
         yield f"g{m}x{k}", rng.standard_normal((m, k))
 

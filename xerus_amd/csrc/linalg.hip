@@ -467,6 +467,7 @@ static void svd_core(xrs_handle_t h, const double* A, size_t m, size_t n, double
     // non-square with 24 <= min(m, n) <= 128: the bidiagonal route on the QR factor (profiles/r06/svd_bidiag_*:
     // 64 x 1000 0.61 vs 5.1 ms, 128 x 2560 1.11 vs 1.71 ms, 300 x 100 0.80 vs 1.45 ms against Jacobi)
     const bool bd = m != n && k >= 24 && k <= 128 && svd_bidiag_mode() != 0;
+    // (square 256 / 512 through the QR factor as well: 5.46 vs 4.94 ms and 17.7 vs 18.6 ms -- no gain, r06)
     if (!bd && m <= n && jacobi_usv_fits(int(m), int(n))) {
         jacobi_svd_rows(h, A, int(m), int(n), U, S, Vt);   // rows of A directly
         return;
