@@ -214,52 +214,6 @@ __global__ void __launch_bounds__(256) k_permute_transpose64(double* __restrict_
     }
 }
 
-// (b'') k_permute_transpose64 with the tile's two 32-row halves pipelined: all 8 loads per thread issued, the
-// first half written to LDS as soon as its 4 loads are in (vmcnt(4)), transposed and stored while the second
-// half's loads are still arriving -- the store phase of one half overlaps the load latency of the other (the
-// mid-size transposes are one tile per CU: load round trip, then store round trip).
-__global__ void __launch_bounds__(256) k_permute_transpose64p(double* __restrict__ out, const double* __restrict__ in, TrArgs a,
-                                                              size_t batch) {
-    __shared__ double tile[TW][TW + 1];
-    const unsigned t = blockIdx.x;
-    const size_t a0 = size_t(t % a.tiles_a) * TW, b0 = size_t(t / a.tiles_a) * TW;
-    const int tx = threadIdx.x & 31;   // load: double2 column within a 64-wide row
-    const int ty = threadIdx.x >> 5;   // 0..7
-    const int sc = threadIdx.x & 15;   // store: double2 column within a 32-wide half row
-    const int sr = threadIdx.x >> 4;   // 0..15
-    for (size_t bi = blockIdx.y; bi < batch; bi += gridDim.y) {
-        unsigned rem = unsigned(bi);
-        size_t ioff = 0, ooff = 0;
-        for (int k = a.nb - 1; k >= 0; --k) {
-            const unsigned dk = unsigned(a.bdims[k]), q = rem / dk, i = rem - q * dk;
-            rem = q;
-            ioff += size_t(i) * a.bin_str[k];
-            ooff += size_t(i) * a.bout_str[k];
-        }
-        dv2 v[TW / 8];
-#pragma unroll
-        for (int j = 0; j < TW / 8; ++j)   // rows b0 + ty + 8 j: j < 4 -> half 0 (rows 0..31), j >= 4 -> half 1
-            v[j] = __builtin_nontemporal_load(reinterpret_cast<const dv2*>(in + ioff + (b0 + ty + 8 * j) * a.in_sb + a0) + tx);
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-            for (int j = 4 * hf; j < 4 * hf + 4; ++j) {
-                tile[ty + 8 * j][2 * tx] = v[j].x;
-                tile[ty + 8 * j][2 * tx + 1] = v[j].y;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {   // output rows a0 + sr + 16 r, columns b0 + 32 hf + 2 sc (+1)
-                dv2 w;
-                w.x = tile[32 * hf + 2 * sc][sr + 16 * r];
-                w.y = tile[32 * hf + 2 * sc + 1][sr + 16 * r];
-                __builtin_nontemporal_store(w, reinterpret_cast<dv2*>(out + ooff + (a0 + sr + 16 * r) * a.out_sa + b0 + 32 * hf) + sc);
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // (c) the same tiled transpose between GROUPS of modes: a = the innermost input modes (contiguous in the
 // input, flattened index fa), b = the innermost output modes (contiguous in the output, index fb). Small
 // modes (the 20^6 reversal: 20 x 20 = 400) then fill whole 32 x 32 tiles instead of 20 x 20 of them.
@@ -437,17 +391,12 @@ void permute(xrs_handle_t h, double* out, const double* in, size_t ndim, const s
     XRS_REQUIRE(tiles < (1ull << 31) && batch < (1ull << 32), "permutation too large");
     const unsigned gy = unsigned(std::min<size_t>(batch, 65535));
     if (wide) {
-        // pipelined halves up to ~4 tiles per CU (1024^2: 4.8 vs 6.1 us, the cfg4 zipper shape 5.9 vs 6.8 us in
-        // alternating runs); above, several workgroups per CU overlap their phases anyway and the half-row stores
-        // cost (4096^2: 54 vs 45 us) -- profiles/r06/permute_pipe_ab_r06.txt
-        const bool pipe = tiles * batch <= 1024;
+        // (r06: the tile's two 32-row halves pipelined -- stores of one half under the other's loads -- measured
+        // 6.1 -> 4.8 us at 1024^2 on one box and 4.9 -> 5.5 us on another, 45 -> 54 us at 4096^2 on both: not kept,
+        // profiles/r06/permute_pipe_ab_r06.txt)
         KernelTimer timer(h, XRS_KFAM_PERMUTE, 0.0, bytes, true);
-        if (pipe)
-            hipExtLaunchKernelGGL(k_permute_transpose64p, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0,
-                                  out, in, ta, batch);
-        else
-            hipExtLaunchKernelGGL(k_permute_transpose64, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0,
-                                  out, in, ta, batch);
+        hipExtLaunchKernelGGL(k_permute_transpose64, dim3(unsigned(tiles), gy), dim3(256), 0, h->stream, timer.start(), timer.stop(), 0,
+                              out, in, ta, batch);
         check_launch("k_permute_transpose64");
         return;
     }
