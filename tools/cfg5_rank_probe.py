@@ -9,6 +9,10 @@ real, certified sharded round whose kernels are those of one rank of an N-way sh
 collectives cost nothing (their volume is printed). N = 1 is cfg5 itself.
 
     python tools/cfg5_rank_probe.py [N ...]       (default 1 2 4 8; N = 0: the unsharded round)
+
+MODE=trunc (r06): the truncating round(256) of the same TT (rank 512 -> 256, the certified truncation);
+MODE=general: the cores graded (column j of every core scaled by 0.97^j) so that the certified truncation refuses
+and round(256) takes the sharded general round (§3.2b). Each call rounds a fresh copy of the slices.
 """
 import math
 import os
@@ -25,6 +29,7 @@ from xerus_amd import dist as xd  # noqa: E402
 
 D, NG, R = 16, 20, 512
 reps = int(os.environ.get("REPS", "6"))
+MODE = os.environ.get("MODE", "chain")   # chain: round(512); trunc / general: round(256)
 h = capi.Handle(0)
 for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
     if world == 0:   # the unsharded single-GPU round of cfg5 (xrs_tt_round), for comparison
@@ -55,21 +60,28 @@ for world in [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]:
         for k in range(D // 2 + 1, D):
             a, _, b = cores[k].shape
             cores[k] = np.linalg.qr(cores[k].reshape(a, m * b).T)[0].T.reshape(a, m, b)
+    if MODE == "general":
+        for k in range(D - 1):
+            cores[k] = cores[k] * (0.97 ** np.arange(cores[k].shape[2]))[None, None, :]
     local = capi.TTDevice.from_cores(h, cores)
     comm = xd.EmulatedComm(h, world)
     ts, paths = [], set()
     st = xd.ShardedTT(h, local, [m * world] * D, world, 0)
     first = st.round_sharded(R, comm)   # canonicalises (as bench.py's cfg5: the timed rounds start right-canonical)
+    target = R if MODE == "chain" else R // 2
     for i in range(reps):
+        c = st if MODE == "chain" else xd.ShardedTT(h, st.local.clone(), st.dims, world, 0)
         c0 = comm.calls
         h.synchronize()
         t0 = time.perf_counter()
-        paths.add(st.round_sharded(R, comm))
+        paths.add(c.round_sharded(target, comm) or "uncertified")
         h.synchronize()
         ts.append(time.perf_counter() - t0)
         calls = comm.calls - c0
+        if c is not st:
+            c.local.free()
     r2 = sum(r * r for r in ranks[1:-1])
-    print(f"N={world}: m={m} local slices, ranks {ranks[1:-1]}, round(512) {1e3 * min(ts):.3f} ms (median "
+    print(f"N={world} [{MODE}]: m={m} local slices, ranks {ranks[1:-1]}, round({target}) {1e3 * min(ts):.3f} ms (median "
           f"{1e3 * sorted(ts)[len(ts) // 2]:.3f}), path {sorted(paths)} (first call {first}), all-reduces per round {calls} "
           f"(sum over ranks of r x r Grams: {8 * r2 / 1e6:.1f} MB per chain pass)", flush=True)
     comm.close()
