@@ -47,6 +47,12 @@ def main():
     d_ref = ref.dot(x, y)
     out["dot_err"] = abs(gx.dot(gy) - d_ref) / nxy
     out["dot_async_err"] = abs(gx.dot_async(gy).result() - d_ref) / nxy
+    # fp32 <x,y> (xrs_tt_dot_f32; ranks divisible by 4 so that XRS_ZIP32 can pick the fused zipper, whose
+    # per-workgroup stamps XRS_ZIP_STAMPS prints)
+    x4 = ref.TT.random_raw(dims, [8, 32, 32, 32, 8], ref.Rng(13))
+    y4 = ref.TT.random_raw(dims, [8, 32, 32, 32, 8], ref.Rng(14))
+    g4x, g4y = capi.TTDevice.from_cores(h, x4.cores), capi.TTDevice.from_cores(h, y4.cores)
+    out["dot32_err"] = abs(g4x.dot_f32(g4y) - ref.dot(x4, y4)) / np.sqrt(ref.dot(x4, x4) * ref.dot(y4, y4))
     # non-truncating round (the certified chain)
     gc = capi.TTDevice.from_cores(h, x.cores)
     gc.round(40)

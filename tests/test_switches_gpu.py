@@ -30,6 +30,7 @@ def _bars(r):
     assert r["gemm_err"] <= 1e-13
     assert r["sgemm_err"] <= 1e-6
     assert r["dot_err"] <= 1e-12 and r["dot_async_err"] <= 1e-12
+    assert r["dot32_err"] <= 1e-6
     assert r["chain_path"] == "chain" and r["chain_err"] <= 1e-10
     assert r["trunc_ranks_ok"] and r["trunc_err_diff"] <= 1e-6
     assert r["graded_ranks_ok"] and r["graded_err_diff"] <= 1e-6
@@ -57,9 +58,11 @@ def _bars(r):
     ({"XRS_SG_XCD_SPLIT": "1"}, lambda r, err: True),                                  # fp32 split-K per XCD
     ({"XRS_REDUCE_SYM": "0"}, lambda r, err: True),                                    # elementwise sym reduce
     ({"XRS_SVD_BIDIAG": "0"}, lambda r, err: True),                                    # Jacobi-only dense SVD
+    ({"XRS_ZIP32": "1"}, lambda r, err: True),                                         # fused zipper front end
+    ({"XRS_ZIP32": "2", "XRS_ZIP_STAMPS": "1"}, lambda r, err: "[zip stamps]" in err),  # fused zipper + stamps
 ], ids=["default", "dot_gate", "gemm_glds", "gemm_cfg", "no_general", "trunc_jacobi", "syev_max", "debug_round",
         "stamps", "sync_debug", "jacobi_no_early", "glds_st2", "sg_target", "sgemm", "glds_xcd_split", "sg_xcd_split",
-        "reduce_sym", "svd_bidiag"])
+        "reduce_sym", "svd_bidiag", "zip32_front", "zip32_stamps"])
 def test_switch(env, check):
     r, err = _probe(env)
     _bars(r)
